@@ -1,0 +1,198 @@
+"""Benchmark: Mpoints/s per denoise iteration (kNN + NVT/PCA + update) at k = 32 on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--points P] [--k 32] [--k-update 8]
+    torchrun --nproc-per-node N ... bench.py --gpus N          (one process per GPU; weak scaling)
+
+Workload (BASELINE.json configs[3], the headline): `xyzrgb_dragon.obj` is a missing blob in the reference, so
+the substitute of BASELINE.md is used -- P (default 10,000,000) area-weighted samples of stanford-bunny.obj
+(data/stanford_bunny_mesh.npz), isotropic Gaussian noise sigma = 0.005 x bbox diagonal, analytic face normals.
+One "step" = one full iteration of Processor.denoise's loop body on device-resident data: kNN(k) against the
+frozen snapshot -> NVT1 + VU smoothing -> NVT2 + classes -> flat (global reduce) / edge / corner updates.
+Excluded (one-time): snapshot/grid build, initial normals, mean edge length l, data synthesis.
+
+Multi-GPU: every rank denoises its own P-point cloud (seed + rank) -- weak scaling, no data-path collective; the
+timed region is bracketed by barrier + synchronize and the max over ranks is reported.  The spatial-slab mode
+with RCCL halo exchange is exercised by tests/test_dist.py.
+
+The JSON line carries `roofline` for the dominant kernel (fused kNN + NVT1, HIP events on its own stream) and
+`cpu_baseline` (the oracle restatement on host cores over a bounded sample; rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "normal-guided-pointcloud-denoiser_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, ROOT)
+
+import pcd_native as nat  # noqa: E402
+from Pointcloud.Modules.Object import Pointcloud, sample_surface  # noqa: E402
+from Pointcloud.Modules.Processor import Processor  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def b_alg_iteration(k, ku):
+    """Algorithmic bytes / point / iteration: 148 + 72k + 60k_u."""
+    return 148 + 72 * k + 60 * ku
+
+
+def b_alg_knn_nvt1(k):
+    """Fused kNN + NVT1 kernel: query xyz 12 + k winners' snapshot xyz 12k + list write 4k (kNN) + current
+    v_j, n_j 24k + own n 12 + f_n write 12 (NVT1, the list and own position come from registers)."""
+    return 12 + 12 * k + 4 * k + 24 * k + 12 + 12
+
+
+def make_cloud(n, seed, dev, sigma_frac=0.005):
+    m = np.load(os.path.join(ROOT, "data", "stanford_bunny_mesh.npz"))
+    v = torch.from_numpy(m["v"]).to(dev)
+    f = torch.from_numpy(m["f"].astype(np.int64)).to(dev)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    pos, nrm = sample_surface(v, f, n, generator=g)
+    diag = float((v.max(0).values - v.min(0).values).norm())
+    pos = pos + sigma_frac * diag * torch.randn(pos.shape, generator=g, device=dev)
+    return pos.contiguous(), nrm.contiguous(), diag
+
+
+def cpu_baseline(k, ku, sample_points, seed=99):
+    """The oracle (numpy/scipy restatement of the reference, cKDTree workers=1) on a bounded sample."""
+    from oracle import pcd_oracle as O
+    threads = os.cpu_count() or 1
+    torch.set_num_threads(threads)
+    pos, nrm, _ = make_cloud(sample_points, seed, torch.device("cpu"))
+    pos, nrm = pos.numpy(), nrm.numpy()
+    knn = O.FrozenKNN(pos)
+    d = 2 * O.mean_edge_length(pos, knn)
+    t0 = time.perf_counter()
+    O.denoise_iteration(pos, nrm, knn, d, k, ku)
+    dt = time.perf_counter() - t0
+    return {"value": round(sample_points / dt / 1e6, 5), "unit": "Mpoints/s", "cores": threads, "kind": "port",
+            "sample": f"1 iteration of the oracle restatement on {sample_points:,} bunny-sampled points "
+                      f"(k={k}, k_u={ku}), scipy cKDTree workers=1, torch intra-op threads={threads}, "
+                      f"{dt:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--points", type=int, default=10_000_000)
+    ap.add_argument("--k", type=int, default=32)
+    ap.add_argument("--k-update", type=int, default=8)
+    ap.add_argument("--cpu-sample", type=int, default=200_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=5, help="extra per-kernel timed iterations (HIP events)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    pos, nrm, diag = make_cloud(args.points, 2 + rank, dev)
+    pc = Pointcloud(pos, nrm)
+    proc = Processor(pc, k_hint=args.k)
+    d = 2 * float(proc.meanEdgeLength())
+    fused = proc._fused_for(max(args.k, args.k_update))
+    fused.load(proc.graph.pos, proc.graph.n)
+    params = nat.make_params(k=args.k, k_update=args.k_update, d=d)
+
+    for _ in range(args.warmup):
+        fused.iterate(params, 1)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fused.iterate(params, 1)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    ms_per_step = elapsed / args.steps * 1e3
+    total_points = args.points * world
+    value = total_points / (ms_per_step / 1e3) / 1e6
+
+    # per-kernel timing (HIP events on the launch stream), outside the timed region
+    fused.set_timing(True)
+    slots = []
+    for _ in range(args.profile_steps):
+        fused.iterate(params, 1)
+        slots.append(fused.timing())
+    fused.set_timing(False)
+    slots = np.asarray(slots)
+    knn_ms = float(np.mean(slots[:, 0])) if len(slots) else float("nan")
+    names = ["knn_nvt1", "nvt2", "flat_phase", "edge_phase", "corner_phase", "swap", "end"]
+    kernel_ms = {names[i]: round(float(np.mean(slots[:, i])), 4) for i in range(min(slots.shape[1], 5))} if len(slots) else {}
+
+    k1_bytes = b_alg_knn_nvt1(args.k) * args.points
+    achieved = k1_bytes / (knn_ms / 1e3) / 1e9 if knn_ms == knn_ms else None
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile))
+            if tj.get("points") == args.points and tj.get("k") == args.k:
+                traffic = tj.get("knn_nvt1_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    iter_alg = b_alg_iteration(args.k, args.k_update) * args.points
+    out = {
+        "metric": "Mpoints/sec per denoise iteration (kNN+PCA+update), k=32, 1/2/4/8 GPU",
+        "value": round(value, 3),
+        "unit": "Mpoints/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: bunny-sampled surface + Gaussian noise (sigma=0.005*bbox), analytic normals, seed 2+rank",
+        "config": {"workload": "configs[3] headline substitute: 10M-pt bunny-sampled cloud (xyzrgb_dragon.obj is a "
+                               "missing blob), k=32, k_u=8, 1 iteration per step",
+                   "points_per_gpu": args.points, "k": args.k, "k_update": args.k_update,
+                   "global_points": total_points, "parallelism": f"replicas x{world}" if world > 1 else "single"},
+        "iterations_per_sec": round(1e3 / ms_per_step, 2),
+        "kernel_ms": kernel_ms,
+        "iteration_roofline": {"bound": "hbm", "alg_bytes_per_point": b_alg_iteration(args.k, args.k_update),
+                               "achieved": round(iter_alg / (ms_per_step / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s",
+                               "frac": round(iter_alg / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "roofline": {"kernel": "k_knn_nvt1", "bound": "hbm",
+                     "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "traffic": traffic, "alg_bytes_per_launch": k1_bytes, "avg_launch_ms": round(knn_ms, 4)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.k, args.k_update, args.cpu_sample)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,161 @@
+/*
+ * pcd.h -- C-ABI of libpcd.so, the MI355X-native (gfx950) hot path of the normal-guided point-cloud denoiser.
+ *
+ * Every entry point takes raw DEVICE pointers + sizes + an opaque hipStream_t (passed as void*), never torch
+ * types.  Calls are stream-ordered; the library never frees caller memory.  Every entry returns an int status
+ * (PCD_OK = 0, negative on error) and pcd_last_error() returns a thread-local description of the last failure.
+ * Numerical guards of the reference (Σw = 0 fallbacks, singular 3x3 masks, displacement clamps) are reproduced
+ * and never raised.
+ *
+ * Reference interface each entry replaces (paths relative to the reference repository root):
+ *   pcd_grid_build / pcd_grid_*    Selector.__init__ KDTree snapshot          Pointcloud/Modules/Selector.py:138-141
+ *   pcd_knn                         Selector.getKNNSelection                   Pointcloud/Modules/Selector.py:235-246
+ *                                   torch_cluster.knn_graph (loop=False)       Pointcloud/Modules/GraphBuilder.py:60-63
+ *                                   torch_geometric.nn.pool.knn (k=1)          Pointcloud/Modules/Utils.py:253-295
+ *   pcd_nvt_csr                     Decompositionor.getBetterFilteredNVT       Pointcloud/Modules/Decompositionor.py:278-300
+ *   pcd_vu_smooth                   Decomposition.getVUSmoothedNormals         Pointcloud/Modules/Decompositionor.py:92-106
+ *   pcd_classify                    Decomposition.getNVTFeatures/getClasses    Pointcloud/Modules/Decompositionor.py:57-69
+ *   pcd_pca_dense                   GraphBuilder.getPVTDecompositionWithKNN    Pointcloud/Modules/GraphBuilder.py:99-111
+ *   pcd_step_csr                    Denoiser.{flat,edge,feature,corner,new,dummy}_step  Pointcloud/Modules/Denoiser.py:26-232
+ *   pcd_edge_length_sum             TorchUtils.averageEdgeLength               Pointcloud/Modules/Utils.py:297-299
+ *   pcd_nn_dist                     TorchUtils.Chamfer/Paper/HausdorffDistance Pointcloud/Modules/Utils.py:253-295
+ *   pcd_mesh_update                 Mesh.updateVertices                        PatchGeneration/Modules/Mesh.py:377-418
+ *   pcd_denoiser_*                  Processor.denoise / getMyFeatureDecomposition / denoiseUntilMinimumError loop body
+ *                                                                              Pointcloud/Modules/Processor.py:110-185
+ *   pcd_orient_normals_mst          GraphBuilder.flipNormals (MST + DFS, host) Pointcloud/Modules/GraphBuilder.py:129-209
+ */
+#ifndef PCD_H
+#define PCD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ status */
+enum {
+    PCD_OK = 0,
+    PCD_ERR_ARG = -1,      /* bad argument (null pointer, size, unsupported k)     -> AssertionError/ValueError */
+    PCD_ERR_OOM = -2,      /* device allocation failed                               */
+    PCD_ERR_HIP = -3,      /* HIP runtime error                                      */
+    PCD_ERR_STATE = -4,    /* object used in the wrong state                          */
+    PCD_ERR_RCCL = -5      /* collective failure (multi-GPU slab mode)                */
+};
+const char* pcd_last_error(void);
+int pcd_version(void);
+/* Largest k supported by the kNN kernels (register top-k lists). */
+int pcd_max_k(void);
+
+/* ------------------------------------------------------------------ frozen snapshot (H1) */
+typedef struct pcd_grid pcd_grid;
+typedef struct {
+    int64_t n;           /* snapshot points                           */
+    int64_t cells;       /* occupied cells                            */
+    int64_t table_slots; /* hash-table slots                          */
+    float cell;          /* cell edge length                          */
+    float origin[3];     /* cell (0,0,0) lower corner                  */
+    int32_t dims[3];     /* cells per axis over the snapshot bbox       */
+} pcd_grid_info_t;
+
+/* Build the kNN index over a private copy of xyz[n][3] (fp32 device rows).  cell <= 0 picks the cell edge
+ * so an occupied cell holds ~k_hint/2 points.  Synchronises `stream` (one-time construction). */
+int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, void* stream, pcd_grid** out);
+int pcd_grid_destroy(pcd_grid* g);
+int pcd_grid_get_info(const pcd_grid* g, pcd_grid_info_t* out);
+/* perm[r] = original index of the r-th point in the grid's spatial (Morton) order; int32 device [n]. */
+int pcd_grid_perm(const pcd_grid* g, int32_t* perm, void* stream);
+
+/* ------------------------------------------------------------------ kNN (H2) */
+/* For each query row q[nq][3] the k nearest snapshot points, ascending (d², index).
+ *   idx_bits    32 or 64: element type of idx_out ([nq][k] row-major)
+ *   sorted_ids  0: indices in the caller's original order, 1: indices in the grid's spatial order
+ *   exclude_self  1: query i is snapshot point i; drop it (torch_cluster.knn_graph loop=False semantics)
+ *   d2_out      nullable fp32 [nq][k] squared distances */
+int pcd_knn(const pcd_grid* g, const float* q, int64_t nq, int k, void* idx_out, int idx_bits, int sorted_ids,
+            int exclude_self, float* d2_out, void* stream);
+
+/* ------------------------------------------------------------------ tensor voting (H5-H7, H15) */
+/* CSR selection: segment r has centre ci[r] and neighbours nbr[off[r] .. off[r+1]); all int64 (torch long). */
+int pcd_nvt_csr(const float* pos, const float* n, int64_t npts, const int64_t* ci, const int64_t* off,
+                const int64_t* nbr, int64_t m, float rho, float* eigval, float* eigvec, void* stream);
+/* eigval [m][3] ascending, eigvec [m][3][3] (columns), n [m][3] -> f_n [m][3] */
+int pcd_vu_smooth(const float* eigval, const float* eigvec, const float* n, int64_t m, float tau, float damp,
+                  float* out, void* stream);
+/* features nullable [m][3] = (planarity, linearity, sphericity); classes int64 [m] */
+int pcd_classify(const float* eigval, int64_t m, float scale, float* features, int64_t* classes, void* stream);
+/* Covariance of the k neighbours nbr[i*k .. i*k+k) about their own mean; eigval [n][3], eigvec [n][3][3]. */
+int pcd_pca_dense(const float* pos, int64_t n, const int64_t* nbr, int k, float* eigval, float* eigvec,
+                  void* stream);
+
+/* ------------------------------------------------------------------ position updates (H9-H12) */
+enum { PCD_STEP_FLAT = 0, PCD_STEP_EDGE = 1, PCD_STEP_FEATURE = 2, PCD_STEP_CORNER = 3, PCD_STEP_NEW = 4,
+       PCD_STEP_DUMMY = 5 };
+/* One Denoiser.*_step over a CSR selection: out [m][3] new positions of the centres.
+ * edge_vectors [npts][3] is required for PCD_STEP_EDGE only.  Uses a device workspace it allocates
+ * internally for the global (flat/new) reductions; stream-ordered. */
+int pcd_step_csr(int kind, const float* pos, const float* n, const float* edge_vectors, int64_t npts,
+                 const int64_t* ci, const int64_t* off, const int64_t* nbr, int64_t m, float d, float alpha,
+                 float* out, void* stream);
+
+/* ------------------------------------------------------------------ metrics (H4, H17) */
+/* sum over rows of ||pos[b[e]] - pos[a[e]]|| in fp64 -> *sum_out (device double) */
+int pcd_edge_length_sum(const float* pos, const int64_t* a, const int64_t* b, int64_t e, double* sum_out,
+                        void* stream);
+/* for each query: squared distance to / index of its nearest snapshot point (k = 1) */
+int pcd_nn_dist(const pcd_grid* g, const float* q, int64_t nq, float* d2_out, int64_t* idx_out, void* stream);
+
+/* ------------------------------------------------------------------ mesh vertex update (H18) */
+/* k Jacobi sweeps of v_i += Σ_{f∋i} Σ_{c∈f} n_f (n_f·(v_c − v_i)) / (3 deg_i), fp64, in place on v [nv][3].
+ * f [nf][3] int64, fn [nf][3] f64, vf/ni = igl vertex_triangle_adjacency (VF [3nf], NI [nv+1]) int64. */
+int pcd_mesh_update(double* v, int64_t nv, const int64_t* f, const double* fn, int64_t nf, const int64_t* vf,
+                    const int64_t* ni, int k, void* stream);
+
+/* ------------------------------------------------------------------ fused denoise loop (H8, H13, H14) */
+typedef struct pcd_denoiser pcd_denoiser;
+typedef struct {
+    int k;               /* feature kNN size (getMyFeatureDecomposition N), reference default 16       */
+    int k_update;        /* update kNN size, reference 8                                                 */
+    float rho;           /* NVT angle threshold, reference 5*pi/12                                       */
+    float tau;           /* VU smoothing eigenvalue threshold, reference 0.3                             */
+    float damp;          /* VU smoothing dampening d, reference 3                                        */
+    float class_scale;   /* planarity scale in getClasses, reference 0.2                                 */
+    float d;             /* displacement clamp (2 * mean edge length in Processor.denoise)              */
+    int nphases;         /* number of (class, step, alpha) phases, Gauss-Seidel in this order           */
+    int phase_class[3];  /* 0 flat, 1 edge, 2 corner                                                     */
+    int phase_kind[3];   /* PCD_STEP_*                                                                   */
+    float phase_alpha[3];
+} pcd_denoise_params;
+
+int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out);
+int pcd_denoiser_destroy(pcd_denoiser* dn);
+/* pos, n: caller rows [N][3] (original order, N = grid n) -> internal spatial order */
+int pcd_denoiser_load(pcd_denoiser* dn, const float* pos, const float* n, void* stream);
+int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iterations, void* stream);
+/* back to original order; any output pointer may be null.  classes int64 [N] and edge vectors [N][3]
+ * are those of the LAST iteration's NVT2; f_n is the last smoothed normal field (= n after iterate). */
+int pcd_denoiser_store(pcd_denoiser* dn, float* pos, float* n, int64_t* classes, float* edge_vectors,
+                       void* stream);
+/* Profiling aid: elapsed ms of each kernel class in the last iterate() when timing was enabled. */
+int pcd_denoiser_set_timing(pcd_denoiser* dn, int enable);
+int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n_written);
+
+/* ------------------------------------------------------------------ normal orientation (host) */
+/* GraphBuilder.flipNormals: Kruskal MST on cost 1-|n_i·n_j| over the directed edge list (a[e] -> b[e],
+ * host int64 arrays), then DFS from argmax z flipping n_dst when n_src·n_dst < cos(7π/12).  HOST memory,
+ * n [npts][3] fp32 modified in place. */
+int pcd_orient_normals_mst(const float* pos, float* n, int64_t npts, const int64_t* a, const int64_t* b,
+                           int64_t e);
+
+/* ------------------------------------------------------------------ host builds of the per-point math */
+/* The exact __host__ __device__ code the kernels run, compiled for the CPU (HOST pointers); for tests.
+ *   t6 [m][6] = (a00, a01, a02, a11, a12, a22) -> w [m][3] ascending, v [m][3][3] columns (LAPACK ssyevd signs) */
+int pcd_host_eigh3(const float* t6, int64_t m, float* w, float* v);
+int pcd_host_vu_smooth(const float* w, const float* v, const float* n, int64_t m, float tau, float damp, float* out);
+/* a9 [m][3][3] row-major, b3 [m][3] -> x3 [m][3], ok [m] (0 when a pivot is exactly zero, x untouched = 0) */
+int pcd_host_solve3(const float* a9, const float* b3, int64_t m, float* x3, int32_t* ok);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCD_H */

@@ -1,0 +1,64 @@
+"""Normal voting tensors (drop-in for Pointcloud/Modules/Decompositionor.py, hot-path subset).
+
+getBetterFilteredNVT -> pcd_nvt_csr: per segment, gather (v_j, n_j), threshold, accumulate the 6 unique entries of
+T, Σw = 0 fallback, in-register 3x3 Jacobi eigen-decomposition (reference Decompositionor.py:278-300).
+Decomposition.getVUSmoothedNormals -> pcd_vu_smooth (:92-106); getNVTFeatures / getClasses -> pcd_classify (:57-69).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+import pcd_native as _nat
+from .Selector import Selection
+from .Utils import GeneralUtils
+
+
+@dataclass
+class Decomposition:
+    eigval: torch.Tensor   # (m, 3) ascending
+    eigvec: torch.Tensor   # (m, 3, 3) columns
+
+    def __post_init__(self):
+        assert self.eigval.dim() == 2 and self.eigval.size(1) == 3 and self.eigval.is_floating_point()
+        assert self.eigvec.dim() == 3 and self.eigvec.size(1) == 3 and self.eigvec.size(2) == 3
+        assert self.eigvec.is_floating_point()
+        assert self.eigval.size(0) == self.eigvec.size(0)
+
+    def __len__(self):
+        return self.eigval.size(0)
+
+    def getNVTFeatures(self):
+        """(planarity, linearity, sphericity) with λ1 ≥ λ2 ≥ λ3."""
+        dev = self.eigval.device
+        _, feat = _nat.classify(_nat.f32(self.eigval), 1.0, want_features=True)
+        feat = feat.to(dev)
+        return feat[:, 0], feat[:, 1], feat[:, 2]
+
+    def getClasses(self, scale: float = 0.2) -> torch.Tensor:
+        """argmax(scale·planarity, linearity, sphericity): 0 flat, 1 edge, 2 corner."""
+        cls, _ = _nat.classify(_nat.f32(self.eigval), scale)
+        return cls.to(self.eigval.device)
+
+    def getVUFeatures(self, tau: float) -> torch.Tensor:
+        return (self.eigval < tau).sum(dim=1) % 3
+
+    def getVUSmoothedNormals(self, n: torch.Tensor, tau: float = 0.3, d: float = 3):
+        """normalize(d·n + Σ_k [λ_k > τ] (e_k·n) e_k)."""
+        out = _nat.vu_smooth(_nat.f32(self.eigval), _nat.f32(self.eigvec), _nat.f32(n), tau, d)
+        return out.to(n.device)
+
+
+class Decompositionor:
+
+    def __init__(self, graph):
+        GeneralUtils.validateAttributes(graph, ["pos"])
+        self.graph = graph
+
+    def getBetterFilteredNVT(self, selection: Selection, _n: torch.Tensor, rho: float = 0.9) -> Decomposition:
+        dev = self.graph.pos.device
+        pos = _nat.f32(self.graph.pos)
+        ev, evec = _nat.nvt_csr(pos, _nat.f32(_n), _nat.i64(selection.i), _nat.i64(selection.slices),
+                                _nat.i64(selection.j), rho)
+        return Decomposition(ev.to(dev), evec.to(dev))

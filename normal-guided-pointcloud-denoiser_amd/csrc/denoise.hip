@@ -1,0 +1,360 @@
+// Fused denoise loop (H8 + H13/H14): the body of Processor.denoise (Pointcloud/Modules/Processor.py:119-139) on
+// persistent device buffers in the grid's spatial (Morton) order.
+//
+// Per iteration:
+//   K1 knn_nvt1   kNN(k) of the current positions against the frozen snapshot, fused with the first tensor vote
+//                 (Decompositionor.getBetterFilteredNVT on n) and VU smoothing -> f_n; writes the kNN list
+//                 column-major [kcap][N] (coalesced per neighbour slot)
+//   K2 nvt2       second vote on f_n -> class (argmax of scaled features) + edge vector (smallest eigenvector)
+//   per phase (Gauss-Seidel across phases, Jacobi within, reference order flat -> edge -> corner):
+//     [flat/new]  rows_sum -> finish_centre -> rows_maxdist   (GLOBAL centre / delta, Denoiser.py:106-107)
+//     K3 phase    class points update from the ping buffer into the pong buffer, the others copy through
+//   n := f_n (pointer swap)
+// The update kNN list (k_u = 8) is the first k_u columns of the k list: same query positions, same snapshot.
+#include <vector>
+
+#include "pcd_knn.h"
+#include "pcd_ops.h"
+
+namespace pcd {
+int knn_cap(int k);
+
+struct ColNb {
+    const int32_t* idx;
+    int64_t n, i;
+    PCD_DEV int64_t operator()(int t) const { return idx[(int64_t)t * n + i]; }
+};
+struct RegNb32 {
+    const int* l;
+    PCD_DEV int64_t operator()(int t) const { return l[t]; }
+};
+
+__global__ void k_load(const float* __restrict__ pos, const float* __restrict__ n, const int32_t* __restrict__ perm,
+                       int64_t N, float4* __restrict__ pos_s, float4* __restrict__ n_s) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    const int64_t i = perm[r];
+    pos_s[r] = make_float4(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2], 0.f);
+    n_s[r] = make_float4(n[3 * i], n[3 * i + 1], n[3 * i + 2], 0.f);
+}
+
+__global__ void k_store(const float4* __restrict__ pos_s, const float4* __restrict__ n_s,
+                        const uint8_t* __restrict__ cls_s, const float4* __restrict__ edge_s,
+                        const int32_t* __restrict__ perm, int64_t N, float* __restrict__ pos, float* __restrict__ n,
+                        int64_t* __restrict__ cls, float* __restrict__ edge) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    const int64_t i = perm[r];
+    if (pos) { const float4 p = pos_s[r]; pos[3 * i] = p.x; pos[3 * i + 1] = p.y; pos[3 * i + 2] = p.z; }
+    if (n) { const float4 p = n_s[r]; n[3 * i] = p.x; n[3 * i + 1] = p.y; n[3 * i + 2] = p.z; }
+    if (cls) cls[i] = cls_s[r];
+    if (edge) { const float4 p = edge_s[r]; edge[3 * i] = p.x; edge[3 * i + 1] = p.y; edge[3 * i + 2] = p.z; }
+}
+
+// K1: kNN + NVT1 + VU smoothing.
+template <int K>
+__global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __restrict__ pos,
+                                                   const float4* __restrict__ nrm, int64_t N, int k, int kstore,
+                                                   float rho, float tau, float damp, int32_t* __restrict__ idx,
+                                                   float4* __restrict__ fn) {
+    const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const float4 p4 = pos[i];
+    const Vec3 vi = v3(p4.x, p4.y, p4.z);
+    TopK<K> tk;
+    knn_search<K>(g, vi, tk);
+    int l[K];
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+        l[t] = tk.idx(t);
+        if (t < kstore) idx[(int64_t)t * N + i] = l[t];
+    }
+    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho);
+    float w[3], V[3][3];
+    eigh3(T, w, V);
+    const float4 n4 = nrm[i];
+    store4(fn, i, vu_smooth(w, V, v3(n4.x, n4.y, n4.z), tau, damp));
+}
+
+// K2: NVT2 on f_n -> classes + edge vectors.
+template <int K>
+__global__ __launch_bounds__(256) void k_nvt2(const float4* __restrict__ pos, const float4* __restrict__ fn,
+                                               const int32_t* __restrict__ idx, int64_t N, int k, float rho,
+                                               float scale, uint8_t* __restrict__ cls, float4* __restrict__ edge) {
+    const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const float4 p4 = pos[i];
+    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{fn}, v3(p4.x, p4.y, p4.z), k, ColNb{idx, N, i}, rho);
+    float w[3], V[3][3];
+    eigh3(T, w, V);
+    cls[i] = (uint8_t)classify(w, scale, nullptr);
+    store4(edge, i, v3(V[0][0], V[1][0], V[2][0]));
+}
+
+struct RedC { double sx, sy, sz, cnt; };
+
+__global__ void k_class_rows_sum(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N, int ku,
+                                 const uint8_t* __restrict__ cls, int c, RedC* __restrict__ part) {
+    double sx = 0, sy = 0, sz = 0, cnt = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        if (cls[i] != c) continue;
+        for (int t = 0; t < ku; ++t) {
+            const float4 v = pos[idx[(int64_t)t * N + i]];
+            sx += v.x; sy += v.y; sz += v.z;
+        }
+        cnt += ku;
+    }
+    __shared__ double s[4][256];
+    s[0][threadIdx.x] = sx; s[1][threadIdx.x] = sy; s[2][threadIdx.x] = sz; s[3][threadIdx.x] = cnt;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w)
+            for (int a = 0; a < 4; ++a) s[a][threadIdx.x] += s[a][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = RedC{s[0][0], s[1][0], s[2][0], s[3][0]};
+}
+
+__global__ void k_class_centre(const RedC* __restrict__ part, int np, float* __restrict__ g) {
+    __shared__ double s[4][256];
+    double a[4] = {0, 0, 0, 0};
+    for (int b = threadIdx.x; b < np; b += blockDim.x) { a[0] += part[b].sx; a[1] += part[b].sy; a[2] += part[b].sz; a[3] += part[b].cnt; }
+    for (int q = 0; q < 4; ++q) s[q][threadIdx.x] = a[q];
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w)
+            for (int q = 0; q < 4; ++q) s[q][threadIdx.x] += s[q][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double c = s[3][0];
+        g[0] = (float)(s[0][0] / c);
+        g[1] = (float)(s[1][0] / c);
+        g[2] = (float)(s[2][0] / c);
+        reinterpret_cast<unsigned int*>(g)[3] = 0u;
+    }
+}
+
+__global__ void k_class_rows_maxdist(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N,
+                                     int ku, const uint8_t* __restrict__ cls, int c, float* __restrict__ g) {
+    const Vec3 ctr = v3(g[0], g[1], g[2]);
+    float mx = 0.f;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        if (cls[i] != c) continue;
+        for (int t = 0; t < ku; ++t) {
+            const float4 v = pos[idx[(int64_t)t * N + i]];
+            mx = fmaxf(mx, sqrtf(sq3(v3(v.x, v.y, v.z) - ctr)));
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(g) + 3, __float_as_uint(mx));
+}
+
+// K3: one Gauss-Seidel phase: points of class c move (reading pin), all others copy through to pout.
+template <int KIND>
+__global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, float4* __restrict__ pout,
+                                                const float4* __restrict__ fn, const float4* __restrict__ edge,
+                                                const int32_t* __restrict__ idx, int64_t N, int ku,
+                                                const uint8_t* __restrict__ cls, int c, const float* __restrict__ g,
+                                                float d, float alpha) {
+    const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const float4 p4 = pin[i];
+    if (cls[i] != c) { pout[i] = p4; return; }
+    const Vec3 vi = v3(p4.x, p4.y, p4.z);
+    const Rows4 P{pin}, F{fn};
+    const ColNb nb{idx, N, i};
+    Vec3 o;
+    if (KIND == PCD_STEP_FLAT) o = step_flat(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
+    else if (KIND == PCD_STEP_EDGE) o = step_edge(P, F, vi, Rows4{edge}(i), ku, nb, d, alpha);
+    else if (KIND == PCD_STEP_FEATURE) o = step_feature<false>(P, F, vi, F(i), ku, nb, 1.f, d, alpha);
+    else if (KIND == PCD_STEP_NEW) o = step_feature<true>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
+    else if (KIND == PCD_STEP_CORNER) o = step_corner(P, F, vi, ku, nb, d, alpha);
+    else o = vi;
+    store4(pout, i, o);
+}
+
+}  // namespace pcd
+
+using namespace pcd;
+
+struct pcd_denoiser {
+    const pcd_grid* g = nullptr;
+    int64_t n = 0;
+    int kcap = 0;                 // columns of the stored kNN list
+    float4 *pos[2] = {nullptr, nullptr}, *nrm = nullptr, *fn = nullptr, *edge = nullptr;
+    int cur = 0;                  // pos[cur] holds the current positions
+    int32_t* idx = nullptr;
+    uint8_t* cls = nullptr;
+    RedC* part = nullptr;
+    float* gscal = nullptr;       // 4 floats per phase: centre xyz, delta bits
+    bool loaded = false, iterated = false;
+    bool timing = false;
+    std::vector<hipEvent_t> ev;
+    std::vector<float> ms;
+};
+
+static const int kNumPart = 1024;
+
+extern "C" {
+
+int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out) {
+    PCD_CHECK_ARG(out != nullptr, "out is null");
+    *out = nullptr;
+    PCD_CHECK_ARG(g != nullptr, "grid is null");
+    PCD_CHECK_ARG(k_max >= 1 && k_max <= pcd_max_k(), "k_max out of range");
+    pcd_denoiser* dn = new pcd_denoiser();
+    dn->g = g;
+    dn->n = g->n;
+    int cap = knn_cap(k_max);
+    if (cap < 8) cap = 8;
+    dn->kcap = k_max;
+    const int64_t N = g->n;
+    bool ok = hipMalloc(&dn->pos[0], N * sizeof(float4)) == hipSuccess &&
+              hipMalloc(&dn->pos[1], N * sizeof(float4)) == hipSuccess &&
+              hipMalloc(&dn->nrm, N * sizeof(float4)) == hipSuccess &&
+              hipMalloc(&dn->fn, N * sizeof(float4)) == hipSuccess &&
+              hipMalloc(&dn->edge, N * sizeof(float4)) == hipSuccess &&
+              hipMalloc(&dn->idx, (int64_t)k_max * N * sizeof(int32_t)) == hipSuccess &&
+              hipMalloc(&dn->cls, N) == hipSuccess &&
+              hipMalloc(&dn->part, kNumPart * sizeof(RedC)) == hipSuccess &&
+              hipMalloc(&dn->gscal, 16 * sizeof(float)) == hipSuccess;
+    if (!ok) {
+        pcd_denoiser_destroy(dn);
+        return fail(PCD_ERR_OOM, "pcd_denoiser_create: device allocation");
+    }
+    *out = dn;
+    return PCD_OK;
+}
+
+int pcd_denoiser_destroy(pcd_denoiser* dn) {
+    if (!dn) return PCD_OK;
+    (void)(void)hipFree(dn->pos[0]); (void)hipFree(dn->pos[1]); (void)hipFree(dn->nrm); (void)hipFree(dn->fn); (void)hipFree(dn->edge);
+    (void)(void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part); (void)hipFree(dn->gscal);
+    for (auto e : dn->ev) (void)hipEventDestroy(e);
+    delete dn;
+    return PCD_OK;
+}
+
+int pcd_denoiser_load(pcd_denoiser* dn, const float* pos, const float* n, void* stream) {
+    PCD_CHECK_ARG(dn && pos && n, "null argument");
+    hipLaunchKernelGGL(k_load, dim3((unsigned)cdiv(dn->n, 256)), dim3(256), 0, as_stream(stream), pos, n,
+                       dn->g->perm, dn->n, dn->pos[0], dn->nrm);
+    PCD_LAUNCH_CHECK();
+    dn->cur = 0;
+    dn->loaded = true;
+    dn->iterated = false;
+    return PCD_OK;
+}
+
+int pcd_denoiser_set_timing(pcd_denoiser* dn, int enable) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    dn->timing = enable != 0;
+    if (dn->timing && dn->ev.empty()) {
+        dn->ev.resize(8);
+        for (auto& e : dn->ev) PCD_HIP(hipEventCreate(&e));
+    }
+    return PCD_OK;
+}
+
+int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n_written) {
+    PCD_CHECK_ARG(dn && ms_out && n_written, "null argument");
+    *n_written = 0;
+    if (!dn->timing || dn->ev.empty()) return PCD_OK;
+    PCD_HIP(hipEventSynchronize(dn->ev.back()));
+    int w = 0;
+    for (size_t s = 0; s + 1 < dn->ev.size() && w < n_slots; ++s) {
+        float m = 0.f;
+        PCD_HIP(hipEventElapsedTime(&m, dn->ev[s], dn->ev[s + 1]));
+        ms_out[w++] = m;
+    }
+    *n_written = w;
+    return PCD_OK;
+}
+
+int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iterations, void* stream) {
+    PCD_CHECK_ARG(dn && p, "null argument");
+    PCD_CHECK_ARG(dn->loaded, "pcd_denoiser_load must be called first");
+    PCD_CHECK_ARG(p->k >= 1 && p->k_update >= 1, "k, k_update must be >= 1");
+    PCD_CHECK_ARG(std::max(p->k, p->k_update) <= dn->kcap, "k / k_update exceed the k_max given at create");
+    PCD_CHECK_ARG(std::max(p->k, p->k_update) <= dn->n, "k exceeds the number of points");
+    PCD_CHECK_ARG(p->nphases >= 0 && p->nphases <= 3, "nphases must be 0..3");
+    for (int ph = 0; ph < p->nphases; ++ph) {
+        PCD_CHECK_ARG(p->phase_class[ph] >= 0 && p->phase_class[ph] <= 2, "phase class must be 0, 1 or 2");
+        PCD_CHECK_ARG(p->phase_kind[ph] >= PCD_STEP_FLAT && p->phase_kind[ph] <= PCD_STEP_DUMMY, "bad phase kind");
+    }
+    hipStream_t st = as_stream(stream);
+    const int64_t N = dn->n;
+    const int kstore = std::max(p->k, p->k_update);
+    const int cap = knn_cap(kstore) < 8 ? 8 : knn_cap(kstore);
+    const dim3 blk(256), grd((unsigned)cdiv(N, 256));
+    const GridView gv = dn->g->view;
+    for (int it = 0; it < iterations; ++it) {
+        const bool rec = dn->timing && it == iterations - 1;
+        if (rec) PCD_HIP(hipEventRecord(dn->ev[0], st));
+        float4* P = dn->pos[dn->cur];
+#define PCD_K1(C) \
+    case C: hipLaunchKernelGGL(k_knn_nvt1<C>, grd, blk, 0, st, gv, P, dn->nrm, N, p->k, kstore, p->rho, p->tau, p->damp, dn->idx, dn->fn); break;
+        switch (cap) {
+            PCD_K1(8) PCD_K1(16) PCD_K1(24) PCD_K1(32) PCD_K1(48) PCD_K1(64)
+            default: return fail(PCD_ERR_ARG, "unsupported k");
+        }
+#undef PCD_K1
+        PCD_LAUNCH_CHECK();
+        if (rec) PCD_HIP(hipEventRecord(dn->ev[1], st));
+#define PCD_K2(C) \
+    case C: hipLaunchKernelGGL(k_nvt2<C>, grd, blk, 0, st, P, dn->fn, dn->idx, N, p->k, p->rho, p->class_scale, dn->cls, dn->edge); break;
+        switch (cap) {
+            PCD_K2(8) PCD_K2(16) PCD_K2(24) PCD_K2(32) PCD_K2(48) PCD_K2(64)
+            default: return fail(PCD_ERR_ARG, "unsupported k");
+        }
+#undef PCD_K2
+        PCD_LAUNCH_CHECK();
+        if (rec) PCD_HIP(hipEventRecord(dn->ev[2], st));
+        for (int ph = 0; ph < p->nphases; ++ph) {
+            const int kind = p->phase_kind[ph], c = p->phase_class[ph];
+            float* gs = dn->gscal + 4 * ph;
+            float4* pin = dn->pos[dn->cur];
+            float4* pout = dn->pos[dn->cur ^ 1];
+            if (kind == PCD_STEP_FLAT || kind == PCD_STEP_NEW) {
+                hipLaunchKernelGGL(k_class_rows_sum, dim3(kNumPart), blk, 0, st, pin, dn->idx, N, p->k_update, dn->cls, c, dn->part);
+                hipLaunchKernelGGL(k_class_centre, dim3(1), blk, 0, st, dn->part, kNumPart, gs);
+                hipLaunchKernelGGL(k_class_rows_maxdist, dim3(kNumPart), blk, 0, st, pin, dn->idx, N, p->k_update, dn->cls, c, gs);
+            }
+            const float a = p->phase_alpha[ph];
+#define PCD_PH(KD) hipLaunchKernelGGL(k_phase<KD>, grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, N, p->k_update, dn->cls, c, gs, p->d, a)
+            switch (kind) {
+                case PCD_STEP_FLAT: PCD_PH(PCD_STEP_FLAT); break;
+                case PCD_STEP_EDGE: PCD_PH(PCD_STEP_EDGE); break;
+                case PCD_STEP_FEATURE: PCD_PH(PCD_STEP_FEATURE); break;
+                case PCD_STEP_CORNER: PCD_PH(PCD_STEP_CORNER); break;
+                case PCD_STEP_NEW: PCD_PH(PCD_STEP_NEW); break;
+                default: PCD_PH(PCD_STEP_DUMMY); break;
+            }
+#undef PCD_PH
+            PCD_LAUNCH_CHECK();
+            dn->cur ^= 1;
+            if (rec) PCD_HIP(hipEventRecord(dn->ev[3 + ph], st));
+        }
+        if (rec)
+            for (int ph = p->nphases; ph < 3; ++ph) PCD_HIP(hipEventRecord(dn->ev[3 + ph], st));
+        std::swap(dn->nrm, dn->fn);   // graph.n = f_n  (Processor.py:139)
+        if (rec) PCD_HIP(hipEventRecord(dn->ev[6], st));
+        if (rec) PCD_HIP(hipEventRecord(dn->ev[7], st));
+        dn->iterated = true;
+    }
+    return PCD_OK;
+}
+
+int pcd_denoiser_store(pcd_denoiser* dn, float* pos, float* n, int64_t* classes, float* edge_vectors,
+                       void* stream) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    PCD_CHECK_ARG(dn->loaded, "nothing loaded");
+    PCD_CHECK_ARG(dn->iterated || (!classes && !edge_vectors), "classes/edge vectors need one iteration");
+    hipLaunchKernelGGL(k_store, dim3((unsigned)cdiv(dn->n, 256)), dim3(256), 0, as_stream(stream), dn->pos[dn->cur],
+                       dn->nrm, dn->cls, dn->edge, dn->g->perm, dn->n, pos, n, classes, edge_vectors);
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+}  // extern "C"

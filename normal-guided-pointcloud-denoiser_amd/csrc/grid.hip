@@ -1,0 +1,355 @@
+// Frozen-snapshot index (H1) and kNN queries (H2, kNN-graph for H15, kNN-1 for H17).
+//
+// Reference: Selector.__init__ builds scipy KDTree(graph.pos) once and never rebuilds it
+// (Pointcloud/Modules/Selector.py:138-141); getKNNSelection queries the CURRENT positions against that
+// snapshot (Selector.py:235-246).  Here: bbox -> cell size -> Morton keys -> radix sort (rocPRIM) -> sorted
+// float4 snapshot + hash of occupied cells.  Build is one-time and synchronises the stream.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include <rocprim/rocprim.hpp>
+
+#include "pcd_knn.h"
+
+namespace pcd {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+// ------------------------------------------------------------------ build kernels
+__global__ void k_bbox(const float* __restrict__ xyz, int64_t n, float* __restrict__ part) {
+    float mn[3] = {3.0e38f, 3.0e38f, 3.0e38f}, mx[3] = {-3.0e38f, -3.0e38f, -3.0e38f};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v = xyz[3 * i + a];
+            mn[a] = fminf(mn[a], v);
+            mx[a] = fmaxf(mx[a], v);
+        }
+    }
+    __shared__ float s[6][256];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { s[a][threadIdx.x] = mn[a]; s[3 + a][threadIdx.x] = mx[a]; }
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                s[a][threadIdx.x] = fminf(s[a][threadIdx.x], s[a][threadIdx.x + w]);
+                s[3 + a][threadIdx.x] = fmaxf(s[3 + a][threadIdx.x], s[3 + a][threadIdx.x + w]);
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = s[threadIdx.x][0];
+}
+
+__global__ void k_sample(const float* __restrict__ xyz, int64_t n, int64_t stride, int64_t s, float* __restrict__ out) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= s) return;
+    const int64_t i = t * stride;
+    out[3 * t] = xyz[3 * i];
+    out[3 * t + 1] = xyz[3 * i + 1];
+    out[3 * t + 2] = xyz[3 * i + 2];
+}
+
+__global__ void k_keys(const float* __restrict__ xyz, int64_t n, float ox, float oy, float oz, float inv_h,
+                       unsigned long long* __restrict__ keys, int32_t* __restrict__ vals) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int cx = cell_coord(xyz[3 * i], ox, inv_h);
+    const int cy = cell_coord(xyz[3 * i + 1], oy, inv_h);
+    const int cz = cell_coord(xyz[3 * i + 2], oz, inv_h);
+    keys[i] = morton3(max(cx, 0), max(cy, 0), max(cz, 0));
+    vals[i] = (int32_t)i;
+}
+
+__global__ void k_gather_sorted(const float* __restrict__ xyz, const int32_t* __restrict__ perm, int64_t n,
+                                float4* __restrict__ pts) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const int64_t i = perm[r];
+    pts[r] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], 0.f);
+}
+
+__global__ void k_count_starts(const unsigned long long* __restrict__ keys, int64_t n, unsigned long long* count) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const bool st = (r < n) && (r == 0 || keys[r] != keys[r - 1]);
+    const unsigned long long b = __ballot(st);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (unsigned long long)__popcll(b));
+}
+
+__global__ void k_insert(const unsigned long long* __restrict__ keys, int64_t n, HashSlot* table, int hbits,
+                         unsigned long long mask) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const unsigned long long key = keys[r];
+    if (r != 0 && keys[r - 1] == key) return;
+    int64_t end = r + 1;
+    while (end < n && keys[end] == key) ++end;
+    unsigned long long slot = hash_slot(key, hbits);
+    for (;;) {
+        unsigned long long prev = atomicCAS(&table[slot].key, kEmptyKey, key);
+        if (prev == kEmptyKey || prev == key) break;
+        slot = (slot + 1) & mask;
+    }
+    table[slot].start = (uint32_t)r;
+    table[slot].end = (uint32_t)end;
+}
+
+// ------------------------------------------------------------------ query kernels
+template <int K, bool IDX64>
+__global__ __launch_bounds__(256) void k_knn(GridView g, const float* __restrict__ q, int64_t nq, int kq, int k,
+                                              void* __restrict__ idx_out, const int32_t* __restrict__ perm,
+                                              int exclude_self, float* __restrict__ d2_out) {
+    const int64_t nb = gridDim.x;
+    const int64_t b = xcd_block(blockIdx.x, nb);
+    const int64_t i = b * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const Vec3 qi = v3(q[3 * i], q[3 * i + 1], q[3 * i + 2]);
+    TopK<K> tk;
+    knn_search<K>(g, qi, tk);
+    int w = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        int id = tk.idx(j);
+        if (perm) id = (j < kq) ? perm[id] : -1;
+        const bool take = (w < k) && (j < kq) && !(exclude_self && id == i);
+        if (take) {
+            if (IDX64) reinterpret_cast<int64_t*>(idx_out)[i * k + w] = id;
+            else reinterpret_cast<int32_t*>(idx_out)[i * k + w] = id;
+            if (d2_out) d2_out[i * k + w] = tk.d2(j);
+            ++w;
+        }
+    }
+}
+
+__global__ void k_nn1(GridView g, const float* __restrict__ q, int64_t nq, const int32_t* __restrict__ perm,
+                      float* __restrict__ d2_out, int64_t* __restrict__ idx_out) {
+    const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    TopK<1> tk;
+    knn_search<1>(g, v3(q[3 * i], q[3 * i + 1], q[3 * i + 2]), tk);
+    if (d2_out) d2_out[i] = tk.d2(0);
+    if (idx_out) idx_out[i] = perm[tk.idx(0)];
+}
+
+// K capacity ladder of the register top-k lists.
+static const int kCaps[] = {1, 4, 8, 13, 16, 24, 32, 48, 64};
+int knn_cap(int k) {
+    for (int c : kCaps)
+        if (k <= c) return c;
+    return -1;
+}
+
+template <bool IDX64>
+static int launch_knn(const GridView& g, const float* q, int64_t nq, int kq, int k, void* idx, const int32_t* perm,
+                      int excl, float* d2, hipStream_t st) {
+    const int cap = knn_cap(kq);
+    const dim3 blk(256), grd((unsigned)cdiv(nq, 256));
+#define PCD_KNN_CASE(C) \
+    case C: hipLaunchKernelGGL((k_knn<C, IDX64>), grd, blk, 0, st, g, q, nq, kq, k, idx, perm, excl, d2); break;
+    switch (cap) {
+        PCD_KNN_CASE(1) PCD_KNN_CASE(4) PCD_KNN_CASE(8) PCD_KNN_CASE(13) PCD_KNN_CASE(16) PCD_KNN_CASE(24)
+        PCD_KNN_CASE(32) PCD_KNN_CASE(48) PCD_KNN_CASE(64)
+        default: return fail(PCD_ERR_ARG, "pcd_knn: k larger than pcd_max_k()");
+    }
+#undef PCD_KNN_CASE
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+// ------------------------------------------------------------------ host: cell size selection
+// Surface-sampled clouds: mean occupancy of a non-empty cell grows like h^2, and a strided sample of S points at
+// cell h_s*sqrt(N/S) has the same occupancy as the full cloud at h_s.  Aim for ~max(2, k_hint/2) points per
+// occupied cell, so the 27-cell block usually holds the k nearest.  Only speed depends on this choice.
+static float choose_cell(const std::vector<float>& smp, int64_t n, const float mn[3], const float mx[3], int k_hint) {
+    const int64_t S = (int64_t)smp.size() / 3;
+    const float target = std::max(2.0f, 0.5f * (float)k_hint);
+    const double ext = std::max({(double)mx[0] - mn[0], (double)mx[1] - mn[1], (double)mx[2] - mn[2], 1e-30});
+    double hs = ext * std::sqrt((double)target / std::max<int64_t>(S, 1));
+    std::vector<unsigned long long> keys((size_t)S);
+    for (int it = 0; it < 4; ++it) {
+        for (int64_t i = 0; i < S; ++i) {
+            unsigned long long c[3];
+            for (int a = 0; a < 3; ++a) c[a] = (unsigned long long)std::floor((smp[3 * i + a] - mn[a]) / hs) & 0x1fffff;
+            keys[i] = c[0] | (c[1] << 21) | (c[2] << 42);
+        }
+        std::sort(keys.begin(), keys.end());
+        const int64_t u = std::unique(keys.begin(), keys.end()) - keys.begin();
+        const double occ = (double)S / (double)std::max<int64_t>(u, 1);
+        const double f = std::sqrt(target / occ);
+        hs *= std::min(std::max(f, 0.25), 4.0);
+        if (std::fabs(f - 1.0) < 0.05) break;
+    }
+    double h = hs * std::sqrt((double)S / (double)std::max<int64_t>(n, 1));
+    // keep every axis within 2^21 cells
+    h = std::max(h, ext / 2000000.0);
+    if (!(h > 0) || !std::isfinite(h)) h = 1.0;
+    return (float)h;
+}
+
+}  // namespace pcd
+
+using namespace pcd;
+
+extern "C" {
+
+const char* pcd_last_error(void) { return g_last_error.c_str(); }
+int pcd_version(void) { return 1; }
+int pcd_max_k(void) { return 64; }
+
+int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, void* stream, pcd_grid** out) {
+    PCD_CHECK_ARG(out != nullptr, "out is null");
+    *out = nullptr;
+    PCD_CHECK_ARG(xyz != nullptr && n > 0, "empty point set");
+    PCD_CHECK_ARG(n < (int64_t)INT32_MAX, "more than 2^31-1 points in one grid");
+    hipStream_t st = as_stream(stream);
+    pcd_grid* g = new pcd_grid();
+    g->n = n;
+    PCD_HIP(hipGetDevice(&g->device));
+    auto cleanup = [&]() { pcd_grid_destroy(g); };
+
+    // bbox
+    const int nbb = 512;
+    float* part = nullptr;
+    if (hipMalloc(&part, nbb * 6 * sizeof(float)) != hipSuccess) { cleanup(); return fail(PCD_ERR_OOM, "bbox"); }
+    hipLaunchKernelGGL(k_bbox, dim3(nbb), dim3(256), 0, st, xyz, n, part);
+    std::vector<float> hp(nbb * 6);
+    (void)hipMemcpyAsync(hp.data(), part, nbb * 6 * sizeof(float), hipMemcpyDeviceToHost, st);
+    // strided sample for the cell-size heuristic
+    const int64_t S = std::min<int64_t>(n, 65536);
+    const int64_t stride = n / S;
+    float* dsmp = nullptr;
+    if (hipMalloc(&dsmp, S * 3 * sizeof(float)) != hipSuccess) { (void)hipFree(part); cleanup(); return fail(PCD_ERR_OOM, "sample"); }
+    hipLaunchKernelGGL(k_sample, dim3((unsigned)cdiv(S, 256)), dim3(256), 0, st, xyz, n, stride, S, dsmp);
+    std::vector<float> smp(S * 3);
+    (void)hipMemcpyAsync(smp.data(), dsmp, S * 3 * sizeof(float), hipMemcpyDeviceToHost, st);
+    hipError_t e = hipStreamSynchronize(st);
+    (void)hipFree(part);
+    (void)hipFree(dsmp);
+    if (e != hipSuccess) { cleanup(); return fail(PCD_ERR_HIP, std::string("grid bbox: ") + hipGetErrorString(e)); }
+    float mn[3], mx[3];
+    for (int a = 0; a < 3; ++a) { mn[a] = 3.0e38f; mx[a] = -3.0e38f; }
+    for (int b = 0; b < nbb; ++b)
+        for (int a = 0; a < 3; ++a) { mn[a] = std::min(mn[a], hp[b * 6 + a]); mx[a] = std::max(mx[a], hp[b * 6 + 3 + a]); }
+    for (int a = 0; a < 3; ++a)
+        if (!std::isfinite(mn[a]) || !std::isfinite(mx[a])) { cleanup(); return fail(PCD_ERR_ARG, "pcd_grid_build: non-finite coordinates"); }
+    float h = cell > 0 ? cell : choose_cell(smp, n, mn, mx, k_hint);
+    for (int a = 0; a < 3; ++a) {
+        const double dimd = std::floor(((double)mx[a] - mn[a]) / h) + 1.0;
+        if (dimd >= 2097151.0) h = (float)(((double)mx[a] - mn[a]) / 2000000.0);
+    }
+    GridView& v = g->view;
+    v.h = h;
+    v.inv_h = 1.0f / h;
+    v.ox = mn[0]; v.oy = mn[1]; v.oz = mn[2];
+    v.dx = (int)std::floor(((double)mx[0] - mn[0]) * v.inv_h) + 2;
+    v.dy = (int)std::floor(((double)mx[1] - mn[1]) * v.inv_h) + 2;
+    v.dz = (int)std::floor(((double)mx[2] - mn[2]) * v.inv_h) + 2;
+    v.n = n;
+
+    // keys + sort
+    unsigned long long *keys = nullptr, *keys2 = nullptr, *cnt = nullptr;
+    int32_t* vals = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    auto free_tmp = [&]() { (void)hipFree(keys); (void)hipFree(keys2); (void)hipFree(vals); (void)hipFree(tmp); (void)hipFree(cnt); };
+    if (hipMalloc(&keys, n * 8) != hipSuccess || hipMalloc(&keys2, n * 8) != hipSuccess ||
+        hipMalloc(&vals, n * 4) != hipSuccess || hipMalloc(&g->perm, n * 4) != hipSuccess ||
+        hipMalloc(&g->pts, n * sizeof(float4)) != hipSuccess || hipMalloc(&cnt, 8) != hipSuccess) {
+        free_tmp(); cleanup(); return fail(PCD_ERR_OOM, "pcd_grid_build: device allocation");
+    }
+    const dim3 blk(256), grd((unsigned)cdiv(n, 256));
+    hipLaunchKernelGGL(k_keys, grd, blk, 0, st, xyz, n, v.ox, v.oy, v.oz, v.inv_h, keys, vals);
+    (void)rocprim::radix_sort_pairs(nullptr, tmp_bytes, keys, keys2, vals, g->perm, (size_t)n, 0u, 63u, st);
+    if (hipMalloc(&tmp, tmp_bytes) != hipSuccess) { free_tmp(); cleanup(); return fail(PCD_ERR_OOM, "sort temp"); }
+    if (rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, keys2, vals, g->perm, (size_t)n, 0u, 63u, st) != hipSuccess) {
+        free_tmp(); cleanup(); return fail(PCD_ERR_HIP, "rocprim::radix_sort_pairs failed");
+    }
+    hipLaunchKernelGGL(k_gather_sorted, grd, blk, 0, st, xyz, g->perm, n, g->pts);
+    (void)hipMemsetAsync(cnt, 0, 8, st);
+    hipLaunchKernelGGL(k_count_starts, grd, blk, 0, st, keys2, n, cnt);
+    unsigned long long cells = 0;
+    (void)hipMemcpyAsync(&cells, cnt, 8, hipMemcpyDeviceToHost, st);
+    e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { free_tmp(); cleanup(); return fail(PCD_ERR_HIP, std::string("grid sort: ") + hipGetErrorString(e)); }
+    g->cells = (int64_t)cells;
+    int hbits = 1;
+    while ((1ll << hbits) < 4 * (int64_t)cells) ++hbits;
+    g->slots = 1ll << hbits;
+    if (hipMalloc(&g->table, g->slots * sizeof(HashSlot)) != hipSuccess) { free_tmp(); cleanup(); return fail(PCD_ERR_OOM, "hash table"); }
+    (void)hipMemsetAsync(g->table, 0xFF, g->slots * sizeof(HashSlot), st);
+    hipLaunchKernelGGL(k_insert, grd, blk, 0, st, keys2, n, g->table, hbits, (unsigned long long)(g->slots - 1));
+    e = hipStreamSynchronize(st);
+    free_tmp();
+    if (e != hipSuccess) { cleanup(); return fail(PCD_ERR_HIP, std::string("grid hash: ") + hipGetErrorString(e)); }
+    v.pts = g->pts;
+    v.table = g->table;
+    v.hbits = hbits;
+    v.mask = (unsigned long long)(g->slots - 1);
+    *out = g;
+    return PCD_OK;
+}
+
+int pcd_grid_destroy(pcd_grid* g) {
+    if (!g) return PCD_OK;
+    (void)hipFree(g->pts);
+    (void)hipFree(g->perm);
+    (void)hipFree(g->table);
+    delete g;
+    return PCD_OK;
+}
+
+int pcd_grid_get_info(const pcd_grid* g, pcd_grid_info_t* out) {
+    PCD_CHECK_ARG(g && out, "null argument");
+    out->n = g->n;
+    out->cells = g->cells;
+    out->table_slots = g->slots;
+    out->cell = g->view.h;
+    out->origin[0] = g->view.ox; out->origin[1] = g->view.oy; out->origin[2] = g->view.oz;
+    out->dims[0] = g->view.dx; out->dims[1] = g->view.dy; out->dims[2] = g->view.dz;
+    return PCD_OK;
+}
+
+int pcd_grid_perm(const pcd_grid* g, int32_t* perm, void* stream) {
+    PCD_CHECK_ARG(g && perm, "null argument");
+    PCD_HIP(hipMemcpyAsync(perm, g->perm, g->n * sizeof(int32_t), hipMemcpyDeviceToDevice, as_stream(stream)));
+    return PCD_OK;
+}
+
+int pcd_knn(const pcd_grid* g, const float* q, int64_t nq, int k, void* idx_out, int idx_bits, int sorted_ids,
+            int exclude_self, float* d2_out, void* stream) {
+    PCD_CHECK_ARG(g != nullptr, "grid is null");
+    PCD_CHECK_ARG(k >= 1 && k <= pcd_max_k(), "k out of range [1, pcd_max_k()]");
+    PCD_CHECK_ARG(idx_bits == 32 || idx_bits == 64, "idx_bits must be 32 or 64");
+    const int kq = k + (exclude_self ? 1 : 0);
+    PCD_CHECK_ARG(kq <= g->n, "k exceeds the number of snapshot points");
+    PCD_CHECK_ARG(kq <= pcd_max_k(), "k (+1 for exclude_self) exceeds pcd_max_k()");
+    if (nq == 0) return PCD_OK;
+    PCD_CHECK_ARG(q && idx_out, "null query / output");
+    PCD_CHECK_ARG(!(exclude_self && sorted_ids), "exclude_self requires original ids");
+    const int32_t* perm = sorted_ids ? nullptr : g->perm;
+    hipStream_t st = as_stream(stream);
+    return idx_bits == 64 ? launch_knn<true>(g->view, q, nq, kq, k, idx_out, perm, exclude_self, d2_out, st)
+                          : launch_knn<false>(g->view, q, nq, kq, k, idx_out, perm, exclude_self, d2_out, st);
+}
+
+int pcd_nn_dist(const pcd_grid* g, const float* q, int64_t nq, float* d2_out, int64_t* idx_out, void* stream) {
+    PCD_CHECK_ARG(g != nullptr, "grid is null");
+    if (nq == 0) return PCD_OK;
+    PCD_CHECK_ARG(q != nullptr, "null query");
+    hipLaunchKernelGGL(k_nn1, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, as_stream(stream), g->view, q, nq,
+                       g->perm, d2_out, idx_out);
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+}  // extern "C"

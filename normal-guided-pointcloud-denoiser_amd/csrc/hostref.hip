@@ -1,0 +1,49 @@
+// Host builds of the per-point math (the same __host__ __device__ source the kernels use), exported so the CPU
+// test-suite can check eigen-decomposition signs, VU smoothing and the 3x3 solve without a GPU.
+#include "pcd_host.h"
+#include "pcd_device.h"
+
+using namespace pcd;
+
+extern "C" {
+
+int pcd_host_eigh3(const float* t6, int64_t m, float* w, float* v) {
+    PCD_CHECK_ARG(t6 && w && v, "null argument");
+    for (int64_t i = 0; i < m; ++i) {
+        const float* a = t6 + 6 * i;
+        float ww[3], V[3][3];
+        eigh3(Sym3{a[0], a[1], a[2], a[3], a[4], a[5]}, ww, V);
+        for (int r = 0; r < 3; ++r) {
+            w[3 * i + r] = ww[r];
+            for (int c = 0; c < 3; ++c) v[9 * i + 3 * r + c] = V[r][c];
+        }
+    }
+    return PCD_OK;
+}
+
+int pcd_host_vu_smooth(const float* w, const float* v, const float* n, int64_t m, float tau, float damp, float* out) {
+    PCD_CHECK_ARG(w && v && n && out, "null argument");
+    for (int64_t i = 0; i < m; ++i) {
+        float V[3][3];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) V[r][c] = v[9 * i + 3 * r + c];
+        const Vec3 f = vu_smooth(w + 3 * i, V, v3(n[3 * i], n[3 * i + 1], n[3 * i + 2]), tau, damp);
+        out[3 * i] = f.x; out[3 * i + 1] = f.y; out[3 * i + 2] = f.z;
+    }
+    return PCD_OK;
+}
+
+int pcd_host_solve3(const float* a9, const float* b3, int64_t m, float* x3, int32_t* ok) {
+    PCD_CHECK_ARG(a9 && b3 && x3 && ok, "null argument");
+    for (int64_t i = 0; i < m; ++i) {
+        float A[3][3];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) A[r][c] = a9[9 * i + 3 * r + c];
+        Vec3 x = v3(0.f, 0.f, 0.f);
+        ok[i] = solve3(A, v3(b3[3 * i], b3[3 * i + 1], b3[3 * i + 2]), x) ? 1 : 0;
+        x3[3 * i] = x.x; x3[3 * i + 1] = x.y; x3[3 * i + 2] = x.z;
+    }
+    return PCD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,419 @@
+// Device-side building blocks shared by every pcd kernel (gfx950 / CDNA4, wave64).
+//
+//  * small fixed-size linear algebra: 3x3 symmetric eigen-decomposition following LAPACK ssyevd step by step
+//    (replaces the reference's batched torch.linalg.eigh, Decompositionor.py:300), 3x3 LU with partial pivoting +
+//    exact-zero-pivot detection (replaces torch.linalg.inv_ex's info mask, Denoiser.py:43-46,80-83,210-214)
+//  * everything is __host__ __device__: libpcd exports host entry points (pcd_host_*) so the exact per-point math
+//    is unit-tested on the CPU as well
+//  * point accessors: the public API hands over caller-owned [n,3] fp32 rows (stride 3), the fused
+//    denoise path keeps float4 rows in HBM (one 16-B load per gathered neighbour)
+//  * XCD-aware block remap: consecutive logical blocks (spatially adjacent points after the Morton
+//    sort) land on the same XCD so neighbour gathers hit that XCD's L2.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PCD_DEV __host__ __device__ __forceinline__
+
+namespace pcd {
+
+struct Vec3 { float x, y, z; };
+
+PCD_DEV Vec3 v3(float x, float y, float z) { return Vec3{x, y, z}; }
+PCD_DEV Vec3 operator+(Vec3 a, Vec3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+PCD_DEV Vec3 operator-(Vec3 a, Vec3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+PCD_DEV Vec3 operator*(float s, Vec3 a) { return v3(s * a.x, s * a.y, s * a.z); }
+// dot in the reference's summation order: (x*x' + y*y') + z*z'  ((a*b).sum(dim=1))
+PCD_DEV float dot3(Vec3 a, Vec3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }  // built with -ffp-contract=off
+PCD_DEV float sq3(Vec3 a) { return dot3(a, a); }
+
+// ---------------------------------------------------------------- point accessors
+// Packed caller rows: float[n*3]
+struct Rows3 {
+    const float* p;
+    PCD_DEV Vec3 operator()(int64_t i) const { const float* q = p + 3 * i; return v3(q[0], q[1], q[2]); }
+};
+// Internal padded rows: float4[n] (w unused / carries an index for the snapshot)
+struct Rows4 {
+    const float4* p;
+    PCD_DEV Vec3 operator()(int64_t i) const { float4 q = p[i]; return v3(q.x, q.y, q.z); }
+};
+
+PCD_DEV void store3(float* out, int64_t i, Vec3 v) { float* q = out + 3 * i; q[0] = v.x; q[1] = v.y; q[2] = v.z; }
+PCD_DEV void store4(float4* out, int64_t i, Vec3 v) { out[i] = make_float4(v.x, v.y, v.z, 0.f); }
+
+// ---------------------------------------------------------------- XCD-aware block mapping
+// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md "Workgroup dispatch"). Remap so
+// that XCD x processes the x-th contiguous slice of logical blocks (speed only, never correctness).
+PCD_DEV int64_t xcd_block(int64_t b, int64_t nb) {
+    const int64_t per = (nb + 7) / 8;
+    const int64_t x = b % 8, w = b / 8;
+    const int64_t full = nb - 8 * (per - 1);  // XCDs 0..full-1 own `per` blocks, the rest per-1
+    int64_t base = (x < full) ? x * per : full * per + (x - full) * (per - 1);
+    return base + w;
+}
+
+// ---------------------------------------------------------------- symmetric 3x3 eigen-decomposition
+// A restatement of what torch.linalg.eigh does on the reference's CPU path for one 3x3 fp32 matrix: LAPACK ssyevd
+// (JOBZ='V', UPLO='L') = ssytd2 Householder tridiagonalisation, ssteqr implicit QL/QR with Wilkinson shifts
+// (compz='I', slaev2 for 2x2 blocks, pre-3.10 slartg sign convention), selection sort, back-transformation by the
+// reflector.  The reference's VU smoothing is NOT invariant to eigenvector signs (Decompositionor.py:101-105 uses
+// Eᵀ·M·E), so the signs must be LAPACK's.  tests/test_capi.py::test_host_eigh_matches_torch checks this code
+// (through pcd_host_eigh3) against MKL's torch.linalg.eigh on the CPU: eigenvalues and every eigenvector sign.
+// Output: ascending eigenvalues w[0] <= w[1] <= w[2]; V[r][k] = component r of eigenvector k.
+struct Sym3 { float a00, a01, a02, a11, a12, a22; };
+
+namespace lapack {
+static constexpr float kEps = 5.9604644775390625e-08f;      // slamch('E') = 2^-24
+static constexpr float kSafmin = 1.17549435e-38f;          // slamch('S')
+static constexpr float kSafmn2 = 4.4408920985006262e-16f;  // 2^-51 (slartg scaling bounds)
+static constexpr float kSafmx2 = 2.2517998136852480e+15f;
+
+PCD_DEV float fsign(float a, float b) { return b >= 0.f ? fabsf(a) : -fabsf(a); }
+PCD_DEV float slapy2(float x, float y) {
+    const float xa = fabsf(x), ya = fabsf(y);
+    const float w = fmaxf(xa, ya), z = fminf(xa, ya);
+    if (z == 0.f || w > 3.4028235e38f) return w;
+    const float q = z / w;
+    return w * sqrtf(1.f + q * q);
+}
+// LAPACK <= 3.9 slartg: r = ±sqrt(f²+g²), c made positive only when |f| > |g|
+PCD_DEV void slartg(float f, float g, float& c, float& s, float& r) {
+    if (g == 0.f) { c = 1.f; s = 0.f; r = f; return; }
+    if (f == 0.f) { c = 0.f; s = 1.f; r = g; return; }
+    float f1 = f, g1 = g;
+    const float scale = fmaxf(fabsf(f1), fabsf(g1));
+    int count = 0;
+    if (scale >= kSafmx2) {
+        do { f1 *= kSafmn2; g1 *= kSafmn2; ++count; } while (fmaxf(fabsf(f1), fabsf(g1)) >= kSafmx2 && count < 20);
+        r = sqrtf(f1 * f1 + g1 * g1);
+        c = f1 / r; s = g1 / r;
+        for (int i = 0; i < count; ++i) r *= kSafmx2;
+    } else if (scale <= kSafmn2) {
+        do { f1 *= kSafmx2; g1 *= kSafmx2; ++count; } while (fmaxf(fabsf(f1), fabsf(g1)) <= kSafmn2 && count < 20);
+        r = sqrtf(f1 * f1 + g1 * g1);
+        c = f1 / r; s = g1 / r;
+        for (int i = 0; i < count; ++i) r *= kSafmn2;
+    } else {
+        r = sqrtf(f1 * f1 + g1 * g1);
+        c = f1 / r; s = g1 / r;
+    }
+    if (fabsf(f) > fabsf(g) && c < 0.f) { c = -c; s = -s; r = -r; }
+}
+// eigensystem of [[a, b], [b, c]]: rt1 (larger |.|), rt2, (cs1, sn1) eigenvector of rt1
+PCD_DEV void slaev2(float a, float b, float c, float& rt1, float& rt2, float& cs1, float& sn1) {
+    const float sm = a + c, df = a - c, adf = fabsf(df), tb = b + b, ab = fabsf(tb);
+    float acmx, acmn;
+    if (fabsf(a) > fabsf(c)) { acmx = a; acmn = c; } else { acmx = c; acmn = a; }
+    float rt;
+    if (adf > ab) { const float q = ab / adf; rt = adf * sqrtf(1.f + q * q); }
+    else if (adf < ab) { const float q = adf / ab; rt = ab * sqrtf(1.f + q * q); }
+    else rt = ab * 1.41421356237309515f;
+    int sgn1, sgn2;
+    if (sm < 0.f) { rt1 = 0.5f * (sm - rt); sgn1 = -1; rt2 = (acmx / rt1) * acmn - (b / rt1) * b; }
+    else if (sm > 0.f) { rt1 = 0.5f * (sm + rt); sgn1 = 1; rt2 = (acmx / rt1) * acmn - (b / rt1) * b; }
+    else { rt1 = 0.5f * rt; rt2 = -0.5f * rt; sgn1 = 1; }
+    float cs;
+    if (df >= 0.f) { cs = df + rt; sgn2 = 1; } else { cs = df - rt; sgn2 = -1; }
+    if (fabsf(cs) > ab) {
+        const float ct = -tb / cs;
+        sn1 = 1.f / sqrtf(1.f + ct * ct);
+        cs1 = ct * sn1;
+    } else if (ab == 0.f) {
+        cs1 = 1.f; sn1 = 0.f;
+    } else {
+        const float tn = -cs / tb;
+        cs1 = 1.f / sqrtf(1.f + tn * tn);
+        sn1 = tn * cs1;
+    }
+    if (sgn1 == sgn2) { const float tn = cs1; cs1 = -sn1; sn1 = tn; }
+}
+// slasr('R', 'V', dir): rotation j acts on columns (j, j+1) of Z, for j in [j0, j0+cnt-1)
+PCD_DEV void rot_cols(float Z[3][3], int j, float ct, float st) {
+    if (ct == 1.f && st == 0.f) return;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float t = Z[i][j + 1];
+        Z[i][j + 1] = ct * t - st * Z[i][j];
+        Z[i][j] = st * t + ct * Z[i][j];
+    }
+}
+
+// ssteqr(compz='I') for n = 3: d[3] diagonal, e[2] off-diagonal -> eigenvalues (ascending) in d, vectors in Z
+PCD_DEV void ssteqr3(float d[3], float e[2], float Z[3][3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Z[i][j] = (i == j) ? 1.f : 0.f;
+    const float eps2 = kEps * kEps;
+    const int nmaxit = 3 * 30;
+    int jtot = 0;
+    int l1 = 0;
+    while (l1 <= 2) {
+        if (l1 > 0) e[l1 - 1] = 0.f;
+        int m = 2;
+        for (int mm = l1; mm < 2; ++mm) {
+            const float tst = fabsf(e[mm]);
+            if (tst == 0.f) { m = mm; break; }
+            if (tst <= (sqrtf(fabsf(d[mm])) * sqrtf(fabsf(d[mm + 1]))) * kEps) { e[mm] = 0.f; m = mm; break; }
+        }
+        int l = l1;
+        const int lsv = l;
+        int lend = m;
+        const int lendsv = lend;
+        l1 = m + 1;
+        if (lend == l) continue;
+        float anorm = 0.f;
+        for (int i = l; i <= lend; ++i) anorm = fmaxf(anorm, fabsf(d[i]));
+        for (int i = l; i < lend; ++i) anorm = fmaxf(anorm, fabsf(e[i]));
+        if (anorm == 0.f) continue;
+        if (fabsf(d[lend]) < fabsf(d[l])) { lend = lsv; l = lendsv; }
+        if (lend > l) {
+            // ---------------- QL iteration
+            for (;;) {
+                int mq = lend;
+                if (l != lend) {
+                    for (int mm = l; mm < lend; ++mm) {
+                        const float tst = fabsf(e[mm]) * fabsf(e[mm]);
+                        if (tst <= (eps2 * fabsf(d[mm])) * fabsf(d[mm + 1]) + kSafmin) { mq = mm; break; }
+                    }
+                }
+                if (mq < lend) e[mq] = 0.f;
+                float p = d[l];
+                if (mq == l) {
+                    d[l] = p; ++l;
+                    if (l <= lend) continue;
+                    break;
+                }
+                if (mq == l + 1) {
+                    float rt1, rt2, c, s;
+                    slaev2(d[l], e[l], d[l + 1], rt1, rt2, c, s);
+                    rot_cols(Z, l, c, s);
+                    d[l] = rt1; d[l + 1] = rt2; e[l] = 0.f; l += 2;
+                    if (l <= lend) continue;
+                    break;
+                }
+                if (jtot == nmaxit) break;
+                ++jtot;
+                float g = (d[l + 1] - p) / (2.f * e[l]);
+                float r = slapy2(g, 1.f);
+                g = d[mq] - p + (e[l] / (g + fsign(r, g)));
+                float s = 1.f, c = 1.f;
+                p = 0.f;
+                float wc[2], ws[2];
+                for (int i = mq - 1; i >= l; --i) {
+                    const float f = s * e[i], b = c * e[i];
+                    slartg(g, f, c, s, r);
+                    if (i != mq - 1) e[i + 1] = r;
+                    g = d[i + 1] - p;
+                    r = (d[i] - g) * s + 2.f * c * b;
+                    p = s * r;
+                    d[i + 1] = g + p;
+                    g = c * r - b;
+                    wc[i - l] = c; ws[i - l] = -s;
+                }
+                for (int j = mq - 1; j >= l; --j) rot_cols(Z, j, wc[j - l], ws[j - l]);   // slasr 'B'
+                d[l] = d[l] - p;
+                e[l] = g;
+            }
+        } else {
+            // ---------------- QR iteration
+            for (;;) {
+                int mq = lend;
+                if (l != lend) {
+                    for (int mm = l; mm > lend; --mm) {
+                        const float tst = fabsf(e[mm - 1]) * fabsf(e[mm - 1]);
+                        if (tst <= (eps2 * fabsf(d[mm])) * fabsf(d[mm - 1]) + kSafmin) { mq = mm; break; }
+                    }
+                }
+                if (mq > lend) e[mq - 1] = 0.f;
+                float p = d[l];
+                if (mq == l) {
+                    d[l] = p; --l;
+                    if (l >= lend) continue;
+                    break;
+                }
+                if (mq == l - 1) {
+                    float rt1, rt2, c, s;
+                    slaev2(d[l - 1], e[l - 1], d[l], rt1, rt2, c, s);
+                    rot_cols(Z, l - 1, c, s);
+                    d[l - 1] = rt1; d[l] = rt2; e[l - 1] = 0.f; l -= 2;
+                    if (l >= lend) continue;
+                    break;
+                }
+                if (jtot == nmaxit) break;
+                ++jtot;
+                float g = (d[l - 1] - p) / (2.f * e[l - 1]);
+                float r = slapy2(g, 1.f);
+                g = d[mq] - p + (e[l - 1] / (g + fsign(r, g)));
+                float s = 1.f, c = 1.f;
+                p = 0.f;
+                float wc[2], ws[2];
+                for (int i = mq; i <= l - 1; ++i) {
+                    const float f = s * e[i], b = c * e[i];
+                    slartg(g, f, c, s, r);
+                    if (i != mq) e[i - 1] = r;
+                    g = d[i] - p;
+                    r = (d[i + 1] - g) * s + 2.f * c * b;
+                    p = s * r;
+                    d[i] = g + p;
+                    g = c * r - b;
+                    wc[i - mq] = c; ws[i - mq] = s;
+                }
+                for (int j = mq; j <= l - 1; ++j) rot_cols(Z, j, wc[j - mq], ws[j - mq]);   // slasr 'F'
+                d[l] = d[l] - p;
+                e[l - 1] = g;
+            }
+        }
+        if (jtot >= nmaxit) break;
+    }
+    // selection sort, ascending (swaps columns of Z)
+    for (int ii = 1; ii < 3; ++ii) {
+        const int i = ii - 1;
+        int k = i;
+        float p = d[i];
+        for (int j = ii; j < 3; ++j)
+            if (d[j] < p) { k = j; p = d[j]; }
+        if (k != i) {
+            d[k] = d[i]; d[i] = p;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) { const float t = Z[r][i]; Z[r][i] = Z[r][k]; Z[r][k] = t; }
+        }
+    }
+}
+}  // namespace lapack
+
+PCD_DEV void eigh3(Sym3 A, float w[3], float V[3][3]) {
+    using namespace lapack;
+    float a22 = A.a11, a32 = A.a12, a33 = A.a22;
+    const float a21 = A.a01, a31 = A.a02;
+    // ssytd2 (UPLO='L'), i = 1: slarfg(2, a21, a31) -> H(1) = I - tau v vᵀ, v = (1, v2) on rows/cols 2..3
+    float tau = 0.f, v2 = 0.f, e1 = a21;
+    if (fabsf(a31) != 0.f) {
+        const float beta = -fsign(slapy2(a21, fabsf(a31)), a21);
+        tau = (beta - a21) / beta;
+        v2 = a31 * (1.f / (a21 - beta));
+        e1 = beta;
+        // x = tau * A22 * v (ssymv, lower), w = x - tau/2 (xᵀv) v, A22 -= v wᵀ + w vᵀ (ssyr2)
+        float y1 = tau * a22;
+        float y2 = tau * a32;
+        y1 = y1 + tau * (a32 * v2);
+        y2 = y2 + (tau * v2) * a33;
+        const float alpha = -0.5f * tau * (y1 + y2 * v2);
+        y1 = y1 + alpha;
+        y2 = y2 + alpha * v2;
+        a22 = a22 - (y1 + y1);
+        a32 = a32 - (v2 * y1 + y2);
+        a33 = a33 - (v2 * y2 + y2 * v2);
+    }
+    float d[3] = {A.a00, a22, a33};
+    float e[2] = {e1, a32};
+    float Z[3][3];
+    ssteqr3(d, e, Z);
+    // sormtr: Z := H(1) Z on rows 2..3
+    if (tau != 0.f) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const float s = Z[1][j] + v2 * Z[2][j];
+            Z[1][j] = Z[1][j] - tau * s;
+            Z[2][j] = Z[2][j] - (tau * s) * v2;
+        }
+    }
+    w[0] = d[0]; w[1] = d[1]; w[2] = d[2];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) V[r][k] = Z[r][k];
+}
+
+// ---------------------------------------------------------------- 3x3 general solve
+// LU with partial pivoting (first max |a| wins, as LAPACK i*amax).  Returns false iff a pivot is exactly
+// zero -- the condition under which torch.linalg.inv_ex reports info != 0.
+PCD_DEV bool solve3(float A[3][3], Vec3 bv, Vec3& x) {
+    float b[3] = {bv.x, bv.y, bv.z};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        int piv = c;
+        float best = fabsf(A[c][c]);
+#pragma unroll
+        for (int r = c + 1; r < 3; ++r) {
+            const float v = fabsf(A[r][c]);
+            if (v > best) { best = v; piv = r; }
+        }
+        if (A[piv][c] == 0.f) return false;
+        if (piv != c) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { float t = A[c][k]; A[c][k] = A[piv][k]; A[piv][k] = t; }
+            float t = b[c]; b[c] = b[piv]; b[piv] = t;
+        }
+        const float inv = 1.f / A[c][c];
+#pragma unroll
+        for (int r = c + 1; r < 3; ++r) {
+            const float f = A[r][c] * inv;
+#pragma unroll
+            for (int k = c; k < 3; ++k) A[r][k] -= f * A[c][k];
+            b[r] -= f * b[c];
+        }
+    }
+    const float x2 = b[2] / A[2][2];
+    const float x1 = (b[1] - A[1][2] * x2) / A[1][1];
+    const float x0 = (b[0] - A[0][1] * x1 - A[0][2] * x2) / A[0][0];
+    x = v3(x0, x1, x2);
+    return true;
+}
+
+// ---------------------------------------------------------------- NVT epilogues
+// Decomposition.getVUSmoothedNormals(n, tau, d)  (Decompositionor.py:92-106), exactly as written there:
+//   E[r][k] = r-th component of the k-th eigenvector in DESCENDING eigenvalue order (stable sort),
+//   M = diag([λ_(r) > τ]) indexed by that same rank r,
+//   f_n = normalize(d·n + Eᵀ M E n)                (normalisation without epsilon)
+// (Eᵀ M E is not the projector E M Eᵀ; with M = I both are the identity.)
+PCD_DEV Vec3 vu_smooth(const float w[3], const float V[3][3], Vec3 n, float tau, float damp) {
+    // stable descending order of the ascending eigenvalues w[0..2]
+    int o[3] = {2, 1, 0};
+    // insertion sort by value descending, ties keep ascending index order
+    int idx[3] = {0, 1, 2};
+#pragma unroll
+    for (int a = 1; a < 3; ++a) {
+#pragma unroll
+        for (int b = a; b > 0; --b) {
+            if (w[idx[b]] > w[idx[b - 1]]) { const int t = idx[b]; idx[b] = idx[b - 1]; idx[b - 1] = t; }
+        }
+    }
+    o[0] = idx[0]; o[1] = idx[1]; o[2] = idx[2];
+    const float nv[3] = {n.x, n.y, n.z};
+    float acc[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const float Er[3] = {V[r][o[0]], V[r][o[1]], V[r][o[2]]};
+        const float u = (Er[0] * nv[0] + Er[1] * nv[1]) + Er[2] * nv[2];
+        const float m = (w[o[r]] > tau) ? 1.f : 0.f;
+        const float mu = m * u;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[c] = acc[c] + mu * Er[c];
+    }
+    const Vec3 nn = v3(damp * n.x + acc[0], damp * n.y + acc[1], damp * n.z + acc[2]);
+    const float len = sqrtf(sq3(nn));
+    return v3(nn.x / len, nn.y / len, nn.z / len);
+}
+
+// Decomposition.getNVTFeatures + getClasses(scale)  (Decompositionor.py:57-69)
+// argmax(scale*planarity, linearity, sphericity); first index wins ties, NaN propagates as in torch.
+PCD_DEV int classify(const float w[3], float scale, float* feat /*nullable, 3*/) {
+    const float l1 = w[2], l2 = w[1], l3 = w[0];
+    const float lin = (l2 - l3) / l1;
+    const float pla = (l1 - l2) / l1;
+    const float sph = l3 / l1;
+    if (feat) { feat[0] = pla; feat[1] = lin; feat[2] = sph; }
+    const float f0 = pla * scale;
+    // torch.argmax treats NaN as the maximum (first NaN wins)
+    if (f0 != f0) return 0;
+    if (lin != lin) return 1;
+    if (sph != sph) return 2;
+    int best = 0; float bv = f0;
+    if (lin > bv) { best = 1; bv = lin; }
+    if (sph > bv) { best = 2; }
+    return best;
+}
+
+}  // namespace pcd

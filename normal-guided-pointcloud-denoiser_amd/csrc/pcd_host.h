@@ -1,0 +1,59 @@
+// Host-side plumbing shared by the libpcd translation units: status/error handling, the grid object, and the
+// device view of the grid that kernels receive by value.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/pcd.h"
+
+namespace pcd {
+
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define PCD_CHECK_ARG(cond, msg) \
+    do { if (!(cond)) return ::pcd::fail(PCD_ERR_ARG, std::string(__func__) + ": " + (msg)); } while (0)
+#define PCD_HIP(call)                                                                                      \
+    do {                                                                                                   \
+        hipError_t e_ = (call);                                                                            \
+        if (e_ != hipSuccess) {                                                                            \
+            return ::pcd::fail(e_ == hipErrorOutOfMemory ? PCD_ERR_OOM : PCD_ERR_HIP,                      \
+                               std::string(__func__) + ": " #call ": " + hipGetErrorString(e_));          \
+        }                                                                                                  \
+    } while (0)
+#define PCD_LAUNCH_CHECK() PCD_HIP(hipGetLastError())
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// One 16-byte hash slot: Morton key of an occupied cell -> [start, end) in the sorted snapshot.
+struct HashSlot {
+    unsigned long long key;
+    uint32_t start, end;
+};
+static constexpr unsigned long long kEmptyKey = ~0ull;
+
+// Kernel-side view of a grid (passed by value).
+struct GridView {
+    const float4* pts;       // snapshot, Morton-sorted, w unused
+    const HashSlot* table;
+    unsigned long long mask; // table slots - 1
+    int hbits;               // log2(slots)
+    float ox, oy, oz, h, inv_h;
+    int dx, dy, dz;
+    int64_t n;
+};
+
+}  // namespace pcd
+
+struct pcd_grid {
+    int device = 0;
+    int64_t n = 0;
+    int64_t cells = 0;
+    float4* pts = nullptr;     // [n]
+    int32_t* perm = nullptr;   // [n] sorted rank -> original index
+    pcd::HashSlot* table = nullptr;
+    int64_t slots = 0;
+    pcd::GridView view{};
+};

@@ -1,0 +1,172 @@
+// Exact k-nearest-neighbour search over the frozen snapshot (replaces scipy KDTree.query on the snapshot
+// taken in Selector.__init__, Pointcloud/Modules/Selector.py:141,243).
+//
+// Index: Morton-sorted snapshot points + an open-addressed hash of occupied cells (GridView).  A query scans
+// its cell and the 26 around it (centre, faces, edges, corners), pruning any cell whose box is farther than
+// the current k-th distance, then expands Chebyshev shells until the k-th distance is provably below the
+// distance to every unscanned cell.  The top-k lives in registers as a sorted list of 64-bit keys
+// (d² bits << 32 | index): fp32 (q-c)² distances (no |q|²+|c|²-2q·c cancellation), ties broken by index.
+#pragma once
+#include "pcd_device.h"
+#include "pcd_host.h"
+
+namespace pcd {
+
+__host__ __device__ inline unsigned long long spread21(unsigned int v) {
+    unsigned long long x = v & 0x1fffffu;
+    x = (x | (x << 32)) & 0x1f00000000ffffull;
+    x = (x | (x << 16)) & 0x1f0000ff0000ffull;
+    x = (x | (x << 8)) & 0x100f00f00f00f00full;
+    x = (x | (x << 4)) & 0x10c30c30c30c30c3ull;
+    x = (x | (x << 2)) & 0x1249249249249249ull;
+    return x;
+}
+__host__ __device__ inline unsigned long long morton3(unsigned int x, unsigned int y, unsigned int z) {
+    return spread21(x) | (spread21(y) << 1) | (spread21(z) << 2);
+}
+__host__ __device__ inline unsigned long long hash_slot(unsigned long long key, int hbits) {
+    return (key * 0x9E3779B97F4A7C15ull) >> (64 - hbits);
+}
+
+PCD_DEV bool cell_range(const GridView& g, int cx, int cy, int cz, uint32_t& s, uint32_t& e) {
+    if ((unsigned)cx >= (unsigned)g.dx || (unsigned)cy >= (unsigned)g.dy || (unsigned)cz >= (unsigned)g.dz)
+        return false;
+    const unsigned long long key = morton3(cx, cy, cz);
+    unsigned long long slot = hash_slot(key, g.hbits);
+    for (;;) {
+        const uint4 sl = *reinterpret_cast<const uint4*>(g.table + slot);
+        const unsigned long long k2 = (unsigned long long)sl.x | ((unsigned long long)sl.y << 32);
+        if (k2 == key) { s = sl.z; e = sl.w; return true; }
+        if (k2 == kEmptyKey) return false;
+        slot = (slot + 1) & g.mask;
+    }
+}
+
+PCD_DEV int cell_coord(float p, float o, float inv_h) {
+    float f = (p - o) * inv_h;
+    f = fminf(fmaxf(f, -1.0e9f), 1.0e9f);  // NaN -> -1e9 (fmaxf drops NaN)
+    return (int)floorf(f);
+}
+
+static constexpr unsigned long long kInfKey = (0x7F800000ull << 32) | 0xFFFFFFFFull;
+
+template <int K>
+struct TopK {
+    unsigned long long key[K];
+    PCD_DEV void init() {
+#pragma unroll
+        for (int i = 0; i < K; ++i) key[i] = kInfKey;
+    }
+    PCD_DEV float kth() const { return __uint_as_float((unsigned)(key[K - 1] >> 32)); }
+    PCD_DEV void insert(unsigned long long c) {
+#pragma unroll
+        for (int j = K - 1; j > 0; --j) {
+            const unsigned long long prev = key[j - 1];
+            const unsigned long long cur = key[j];
+            key[j] = (c < prev) ? prev : ((c < cur) ? c : cur);
+        }
+        key[0] = (c < key[0]) ? c : key[0];
+    }
+    PCD_DEV int idx(int j) const { return (int)(uint32_t)(key[j] & 0xFFFFFFFFull); }
+    PCD_DEV float d2(int j) const { return __uint_as_float((unsigned)(key[j] >> 32)); }
+};
+
+PCD_DEV float dist2(Vec3 q, float4 p) {
+    const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
+    return __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
+}
+
+template <int K>
+PCD_DEV void scan_range(const float4* __restrict__ pts, uint32_t s, uint32_t e, Vec3 q, TopK<K>& tk) {
+    uint32_t r = s;
+    for (; r + 1 < e; r += 2) {  // two loads in flight per lane
+        const float4 p0 = pts[r], p1 = pts[r + 1];
+        const unsigned long long c0 = ((unsigned long long)__float_as_uint(dist2(q, p0)) << 32) | r;
+        const unsigned long long c1 = ((unsigned long long)__float_as_uint(dist2(q, p1)) << 32) | (r + 1);
+        if (c0 < tk.key[K - 1]) tk.insert(c0);
+        if (c1 < tk.key[K - 1]) tk.insert(c1);
+    }
+    if (r < e) {
+        const float4 p0 = pts[r];
+        const unsigned long long c0 = ((unsigned long long)__float_as_uint(dist2(q, p0)) << 32) | r;
+        if (c0 < tk.key[K - 1]) tk.insert(c0);
+    }
+}
+
+PCD_DEV float axis_gap(float q, float lo, float hi) { return fmaxf(fmaxf(lo - q, q - hi), 0.f); }
+
+// Scan one cell unless its box is provably farther than the current k-th candidate.
+template <int K>
+PCD_DEV void visit_cell(const GridView& g, Vec3 q, int cx, int cy, int cz, TopK<K>& tk) {
+    const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
+    const float gx = axis_gap(q.x, lx, lx + g.h), gy = axis_gap(q.y, ly, ly + g.h), gz = axis_gap(q.z, lz, lz + g.h);
+    const float box = gx * gx + gy * gy + gz * gz;
+    if (box > tk.kth() * 1.00001f + 1e-30f) return;
+    uint32_t s, e;
+    if (cell_range(g, cx, cy, cz, s, e)) scan_range<K>(g.pts, s, e, q, tk);
+}
+
+// 3x3x3 neighbourhood: centre, 6 faces, 12 edges, 8 corners (closest cells first -> the k-th distance
+// tightens early and the far cells are pruned).
+__constant__ static const signed char kRing1[27][3] = {
+    {0, 0, 0},
+    {-1, 0, 0}, {1, 0, 0}, {0, -1, 0}, {0, 1, 0}, {0, 0, -1}, {0, 0, 1},
+    {-1, -1, 0}, {1, -1, 0}, {-1, 1, 0}, {1, 1, 0}, {-1, 0, -1}, {1, 0, -1}, {-1, 0, 1}, {1, 0, 1},
+    {0, -1, -1}, {0, 1, -1}, {0, -1, 1}, {0, 1, 1},
+    {-1, -1, -1}, {1, -1, -1}, {-1, 1, -1}, {1, 1, -1}, {-1, -1, 1}, {1, -1, 1}, {-1, 1, 1}, {1, 1, 1}};
+
+// After scanning the Chebyshev block of radius R around (cx,cy,cz): is the top-k final?
+PCD_DEV bool search_done(const GridView& g, Vec3 q, int cx, int cy, int cz, int R, float kth) {
+    bool exhausted = true;
+    float bound = 3.0e38f;
+    const int c[3] = {cx, cy, cz};
+    const int dm[3] = {g.dx, g.dy, g.dz};
+    const float o[3] = {g.ox, g.oy, g.oz};
+    const float qa[3] = {q.x, q.y, q.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (c[a] - R > 0) {
+            exhausted = false;
+            bound = fminf(bound, fmaxf(qa[a] - (o[a] + (c[a] - R) * g.h), 0.f));
+        }
+        if (c[a] + R < dm[a] - 1) {
+            exhausted = false;
+            bound = fminf(bound, fmaxf((o[a] + (c[a] + R + 1) * g.h) - qa[a], 0.f));
+        }
+    }
+    return exhausted || kth <= bound * bound * 0.99998f;
+}
+
+// Exact top-K of the snapshot for query q.
+template <int K>
+PCD_DEV void knn_search(const GridView& g, Vec3 q, TopK<K>& tk) {
+    tk.init();
+    int cx = min(max(cell_coord(q.x, g.ox, g.inv_h), 0), g.dx - 1);
+    int cy = min(max(cell_coord(q.y, g.oy, g.inv_h), 0), g.dy - 1);
+    int cz = min(max(cell_coord(q.z, g.oz, g.inv_h), 0), g.dz - 1);
+#pragma unroll 1
+    for (int t = 0; t < 27; ++t)
+        visit_cell<K>(g, q, cx + kRing1[t][0], cy + kRing1[t][1], cz + kRing1[t][2], tk);
+    int R = 1;
+#pragma unroll 1
+    while (!search_done(g, q, cx, cy, cz, R, tk.kth())) {
+        ++R;
+        if (R > 24) {  // pathological outlier: exhaustive scan (correct, slow, never hit on denoise inputs)
+            tk.init();
+            scan_range<K>(g.pts, 0, (uint32_t)g.n, q, tk);
+            return;
+        }
+#pragma unroll 1
+        for (int dz = -R; dz <= R; ++dz) {
+#pragma unroll 1
+            for (int dy = -R; dy <= R; ++dy) {
+                const bool rim = (dz == -R || dz == R || dy == -R || dy == R);
+                const int step = rim ? 1 : 2 * R;
+#pragma unroll 1
+                for (int dx = -R; dx <= R; dx += step) visit_cell<K>(g, q, cx + dx, cy + dy, cz + dz, tk);
+            }
+        }
+    }
+}
+
+}  // namespace pcd

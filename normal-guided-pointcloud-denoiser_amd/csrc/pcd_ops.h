@@ -1,0 +1,191 @@
+// Per-point math of the reference's tensor-voting and position-update operators, written once as device
+// functions over an abstract neighbour list (nb(t) -> point index) so that the public CSR kernels (one call per
+// reference method) and the fused denoise kernels (dense column-major kNN lists) share one implementation.
+#pragma once
+#include "pcd_device.h"
+
+namespace pcd {
+
+// ----------------------------------------------------------------- H5: Decompositionor.getBetterFilteredNVT
+// w_ij = acos(|clamp(normalize(v_j - v_i) . n_j, -1, 1)|) > rho       (Decompositionor.py:290; F.normalize eps 1e-12)
+// T_i  = Σ w n_j n_jᵀ / Σ w,  all w := 1 when Σ w = 0                 (Decompositionor.py:291-299)
+// UNROLL > 0: the neighbour loop is fully unrolled to UNROLL (>= cnt) so register-resident neighbour lists stay
+// in registers and every gather of the list can be issued before the first is consumed.
+template <int UNROLL = 0, class P, class Nr, class Nb>
+PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho) {
+    float w00 = 0.f, w01 = 0.f, w02 = 0.f, w11 = 0.f, w12 = 0.f, w22 = 0.f;
+    float u00 = 0.f, u01 = 0.f, u02 = 0.f, u11 = 0.f, u12 = 0.f, u22 = 0.f;
+    int wsum = 0;
+    auto body = [&](int t) {
+        const int64_t j = nb(t);
+        const Vec3 vj = pos(j), nj = nrm(j);
+        const Vec3 dv = vj - vi;
+        const float den = fmaxf(sqrtf(sq3(dv)), 1e-12f);
+        const Vec3 dn = v3(dv.x / den, dv.y / den, dv.z / den);
+        float c = dot3(dn, nj);
+        c = fabsf(fminf(fmaxf(c, -1.f), 1.f));
+        const bool w = acosf(c) > rho;
+        const float o00 = nj.x * nj.x, o01 = nj.x * nj.y, o02 = nj.x * nj.z;
+        const float o11 = nj.y * nj.y, o12 = nj.y * nj.z, o22 = nj.z * nj.z;
+        u00 += o00; u01 += o01; u02 += o02; u11 += o11; u12 += o12; u22 += o22;
+        if (w) { w00 += o00; w01 += o01; w02 += o02; w11 += o11; w12 += o12; w22 += o22; ++wsum; }
+    };
+    if constexpr (UNROLL > 0) {
+#pragma unroll
+        for (int t = 0; t < UNROLL; ++t)
+            if (t < cnt) body(t);
+    } else {
+        for (int t = 0; t < cnt; ++t) body(t);
+    }
+    Sym3 T;
+    if (wsum == 0) {
+        const float c = (float)cnt;
+        T = Sym3{u00 / c, u01 / c, u02 / c, u11 / c, u12 / c, u22 / c};
+    } else {
+        const float c = (float)wsum;
+        T = Sym3{w00 / c, w01 / c, w02 / c, w11 / c, w12 / c, w22 / c};
+    }
+    return T;
+}
+
+// ----------------------------------------------------------------- H15: GraphBuilder.getPVTDecompositionWithKNN
+// C_i = Σ_j (v_j - v̄)(v_j - v̄)ᵀ with v̄ the mean of the k neighbours (GraphBuilder.py:105-110)
+template <class P, class Nb>
+PCD_DEV Sym3 pca_cov(P pos, int cnt, Nb nb) {
+    float sx = 0.f, sy = 0.f, sz = 0.f;
+    for (int t = 0; t < cnt; ++t) { const Vec3 v = pos(nb(t)); sx += v.x; sy += v.y; sz += v.z; }
+    const float c = (float)cnt;
+    const Vec3 m = v3(sx / c, sy / c, sz / c);
+    Sym3 C{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < cnt; ++t) {
+        const Vec3 d = pos(nb(t)) - m;
+        C.a00 += d.x * d.x; C.a01 += d.x * d.y; C.a02 += d.x * d.z;
+        C.a11 += d.y * d.y; C.a12 += d.y * d.z; C.a22 += d.z * d.z;
+    }
+    return C;
+}
+
+// ----------------------------------------------------------------- helpers for the position updates
+PCD_DEV Vec3 outer_mul(Vec3 a, Vec3 v) {  // (a aᵀ) v, einsum("nij,nj->ni") row order
+    return v3((a.x * a.x) * v.x + (a.x * a.y) * v.y + (a.x * a.z) * v.z,
+              (a.y * a.x) * v.x + (a.y * a.y) * v.y + (a.y * a.z) * v.z,
+              (a.z * a.x) * v.x + (a.z * a.y) * v.y + (a.z * a.z) * v.z);
+}
+PCD_DEV void add_outer(float A[3][3], Vec3 a, float s = 1.f) {
+    const float c[3] = {a.x, a.y, a.z};
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) A[r][q] += s * (c[r] * c[q]);
+}
+// di = α(x - v_i); accept if ||di|| < d (strict; flat_step uses <=)
+PCD_DEV Vec3 clamp_step(Vec3 vi, Vec3 x, float alpha, float d) {
+    const Vec3 di = v3((x.x - vi.x) * alpha, (x.y - vi.y) * alpha, (x.z - vi.z) * alpha);
+    const float nrm = sqrtf(sq3(di));
+    return (nrm < d) ? vi + di : vi;
+}
+
+// ----------------------------------------------------------------- H9: Denoiser.flat_step (Denoiser.py:90-119)
+// delta is the GLOBAL max ||v_j - centre|| over every row of the selection (computed by the caller).
+template <class P, class Nr, class Nb>
+PCD_DEV Vec3 step_flat(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float delta, float d, float alpha) {
+    const float dd = delta * delta;
+    float sx = 0.f, sy = 0.f, sz = 0.f, ws = 0.f;
+    for (int t = 0; t < cnt; ++t) {
+        const int64_t j = nb(t);
+        const Vec3 vj = pos(j), nj = nrm(j);
+        const Vec3 dist = vj - vi;
+        const float sim = expf((-16.f * sq3(ni - nj)) / dd);
+        const float clo = expf((-4.f * sq3(dist)) / dd);
+        const float W = sim * clo;
+        const float wd = W * dot3(nj, dist);
+        sx += wd * ni.x; sy += wd * ni.y; sz += wd * ni.z;
+        ws += W;
+    }
+    const Vec3 di = v3(sx / ws * alpha, sy / ws * alpha, sz / ws * alpha);
+    const float nrm2 = sqrtf(sq3(di));
+    return (nrm2 <= d) ? vi + di : vi;   // NaN (Σ W = 0) -> no move, as di[~mask] = 0
+}
+
+// ----------------------------------------------------------------- H10: Denoiser.edge_step (Denoiser.py:53-88)
+template <class P, class Nr, class Nb>
+PCD_DEV Vec3 step_edge(P pos, Nr nrm, Vec3 vi, Vec3 y, int cnt, Nb nb, float d, float alpha) {
+    float A[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    Vec3 b = v3(0.f, 0.f, 0.f);
+    const Vec3 yyvi = outer_mul(y, vi);
+    const float yc[3] = {y.x, y.y, y.z};
+    for (int t = 0; t < cnt; ++t) {
+        const int64_t j = nb(t);
+        const Vec3 vj = pos(j), nj = nrm(j);
+        const Vec3 vjp = vj - dot3(vj - vi, y) * y;
+        const Vec3 njp = nj - dot3(nj, y) * y;
+        const float nc[3] = {njp.x, njp.y, njp.z};
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) A[r][q] += nc[r] * nc[q] + yc[r] * yc[q];
+        b = b + (outer_mul(njp, vjp) + yyvi);
+    }
+    Vec3 x;
+    if (!solve3(A, b, x)) x = vi;
+    return clamp_step(vi, x, alpha, d);
+}
+
+// ----------------------------------------------------------------- H11: Denoiser.feature_step (Denoiser.py:174-219)
+//                                 and H12: Denoiser.new_step (Denoiser.py:121-172; WEIGHTED=true)
+template <bool WEIGHTED, class P, class Nr, class Nb>
+PCD_DEV Vec3 step_feature(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float delta, float d, float alpha) {
+    float S[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};  // Σ w nj njᵀ
+    Vec3 svj = v3(0.f, 0.f, 0.f);                                       // Σ w vj
+    Vec3 snv = v3(0.f, 0.f, 0.f);                                       // Σ w (nj njᵀ) vj
+    const float dd = delta * delta;
+    for (int t = 0; t < cnt; ++t) {
+        const int64_t j = nb(t);
+        const Vec3 vj = pos(j), nj = nrm(j);
+        float w = 1.f;
+        if (WEIGHTED) {
+            const float dt = dot3(nj, vj - vi);
+            w = expf((-9.f * (dt * dt)) / dd);
+        }
+        const float nc[3] = {nj.x, nj.y, nj.z};
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) S[r][q] += WEIGHTED ? w * (nc[r] * nc[q]) : (nc[r] * nc[q]);
+        svj = svj + (WEIGHTED ? w * vj : vj);
+        const Vec3 nv = outer_mul(nj, vj);
+        snv = snv + (WEIGHTED ? w * nv : nv);
+    }
+    const float nc[3] = {ni.x, ni.y, ni.z};
+    const float card = (float)cnt;
+    float A[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const float no = nc[r] * nc[q];
+            A[r][q] = (((r == q ? 1.f : 0.f) + no) + S[r][q]) + card * no;
+        }
+    const Vec3 b = ((vi + outer_mul(ni, vi)) + outer_mul(ni, svj)) + snv;
+    Vec3 x;
+    if (!solve3(A, b, x)) x = vi;
+    return clamp_step(vi, x, alpha, d);
+}
+
+// ----------------------------------------------------------------- H12: Denoiser.corner_step (Denoiser.py:26-51)
+template <class P, class Nr, class Nb>
+PCD_DEV Vec3 step_corner(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float d, float alpha) {
+    float A[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    Vec3 b = v3(0.f, 0.f, 0.f);
+    for (int t = 0; t < cnt; ++t) {
+        const int64_t j = nb(t);
+        const Vec3 vj = pos(j), nj = nrm(j);
+        add_outer(A, nj);
+        b = b + outer_mul(nj, vj);
+    }
+    Vec3 x;
+    if (!solve3(A, b, x)) x = vi;
+    return clamp_step(vi, x, alpha, d);
+}
+
+}  // namespace pcd

@@ -1,0 +1,330 @@
+"""ctypes binding of ``libpcd.so`` -- the C-ABI declared in ``include/pcd.h``.
+
+This is the only module that talks to the native library.  Every compute call of the drop-in classes under
+``Pointcloud/Modules`` and ``PatchGeneration/Modules`` goes through here and runs a hand-written HIP kernel on the
+current HIP device.  There is NO CPU fallback: if the library or a HIP device is missing, the call raises.
+PyTorch is used for device memory, dtype/shape plumbing and the current stream only.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_float, c_int, c_int64, c_void_p
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PCD_LIB", os.path.join(os.path.dirname(_HERE), "libpcd.so"))
+
+PCD_OK, PCD_ERR_ARG, PCD_ERR_OOM, PCD_ERR_HIP, PCD_ERR_STATE, PCD_ERR_RCCL = 0, -1, -2, -3, -4, -5
+STEP_FLAT, STEP_EDGE, STEP_FEATURE, STEP_CORNER, STEP_NEW, STEP_DUMMY = range(6)
+
+
+class PcdError(RuntimeError):
+    """A native call failed (HIP error, OOM, bad state)."""
+
+
+class _GridInfo(ctypes.Structure):
+    _fields_ = [("n", c_int64), ("cells", c_int64), ("table_slots", c_int64), ("cell", c_float),
+                ("origin", c_float * 3), ("dims", ctypes.c_int32 * 3)]
+
+
+class DenoiseParams(ctypes.Structure):
+    """Mirror of ``pcd_denoise_params`` (include/pcd.h)."""
+    _fields_ = [("k", c_int), ("k_update", c_int), ("rho", c_float), ("tau", c_float), ("damp", c_float),
+                ("class_scale", c_float), ("d", c_float), ("nphases", c_int), ("phase_class", c_int * 3),
+                ("phase_kind", c_int * 3), ("phase_alpha", c_float * 3)]
+
+
+# name -> (restype, argtypes); the exact export list of include/pcd.h
+_SIGS = {
+    "pcd_last_error": (ctypes.c_char_p, []),
+    "pcd_version": (c_int, []),
+    "pcd_max_k": (c_int, []),
+    "pcd_grid_build": (c_int, [c_void_p, c_int64, c_int, c_float, c_void_p, POINTER(c_void_p)]),
+    "pcd_grid_destroy": (c_int, [c_void_p]),
+    "pcd_grid_get_info": (c_int, [c_void_p, POINTER(_GridInfo)]),
+    "pcd_grid_perm": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "pcd_knn": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "pcd_nvt_csr": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p,
+                            c_void_p, c_void_p]),
+    "pcd_vu_smooth": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p, c_void_p]),
+    "pcd_classify": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p, c_void_p]),
+    "pcd_pca_dense": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "pcd_step_csr": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
+                             c_float, c_float, c_void_p, c_void_p]),
+    "pcd_edge_length_sum": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "pcd_nn_dist": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "pcd_mesh_update": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
+    "pcd_denoiser_create": (c_int, [c_void_p, c_int, POINTER(c_void_p)]),
+    "pcd_denoiser_destroy": (c_int, [c_void_p]),
+    "pcd_denoiser_load": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pcd_denoiser_iterate": (c_int, [c_void_p, POINTER(DenoiseParams), c_int, c_void_p]),
+    "pcd_denoiser_store": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pcd_denoiser_set_timing": (c_int, [c_void_p, c_int]),
+    "pcd_denoiser_get_timing": (c_int, [c_void_p, POINTER(c_float), c_int, POINTER(c_int)]),
+    "pcd_orient_normals_mst": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64]),
+    "pcd_host_eigh3": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "pcd_host_vu_smooth": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p]),
+    "pcd_host_solve3": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libpcd.so once (raises ImportError with the build hint if it is missing)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"pcd: native library not found at {LIB_PATH}; run `python -c 'import __graft_entry__ as g; g.build()'` "
+                              "or `make -C normal-guided-pointcloud-denoiser_amd/csrc`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS.keys())
+
+
+def check(status: int, what: str = ""):
+    if status == PCD_OK:
+        return
+    msg = lib().pcd_last_error().decode(errors="replace")
+    if status == PCD_ERR_ARG:
+        raise ValueError(f"pcd: {what}: {msg}")
+    raise PcdError(f"pcd: {what} failed ({status}): {msg}")
+
+
+# ----------------------------------------------------------------------------------------------- device plumbing
+def device() -> torch.device:
+    """The HIP device every kernel runs on.  Raises if there is none (no CPU fallback)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("pcd: no HIP (ROCm) device available -- the denoiser runs its kernels on MI355X only")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t: torch.Tensor | None):
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def on_device(t: torch.Tensor, dtype=None) -> torch.Tensor:
+    """Contiguous copy/view of `t` on the HIP device with the requested dtype."""
+    dev = device()
+    if dtype is not None and t.dtype != dtype:
+        t = t.to(dtype)
+    if t.device != dev:
+        t = t.to(dev, non_blocking=False)
+    return t.contiguous()
+
+
+def f32(t):
+    return on_device(t, torch.float32)
+
+
+def i64(t):
+    return on_device(t, torch.int64)
+
+
+# ----------------------------------------------------------------------------------------------- objects
+class Grid:
+    """Frozen snapshot + kNN index (pcd_grid).  Mirrors the KDTree made in Selector.__init__."""
+
+    def __init__(self, xyz: torch.Tensor, k_hint: int = 16, cell: float = 0.0):
+        L = lib()
+        x = f32(xyz)
+        assert x.dim() == 2 and x.size(1) == 3
+        self._keep = x
+        h = c_void_p()
+        check(L.pcd_grid_build(ptr(x), x.size(0), int(k_hint), float(cell), c_void_p(stream_ptr()), ctypes.byref(h)),
+              "pcd_grid_build")
+        self.handle = h
+        self.n = x.size(0)
+        self._keep = None
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.pcd_grid_destroy(h)
+            self.handle = None
+
+    def info(self) -> dict:
+        gi = _GridInfo()
+        check(lib().pcd_grid_get_info(self.handle, ctypes.byref(gi)), "pcd_grid_get_info")
+        return {"n": gi.n, "cells": gi.cells, "table_slots": gi.table_slots, "cell": gi.cell,
+                "origin": list(gi.origin), "dims": list(gi.dims)}
+
+    def perm(self) -> torch.Tensor:
+        out = torch.empty(self.n, dtype=torch.int32, device=device())
+        check(lib().pcd_grid_perm(self.handle, ptr(out), c_void_p(stream_ptr())), "pcd_grid_perm")
+        return out
+
+    def knn(self, q: torch.Tensor, k: int, exclude_self: bool = False, with_d2: bool = False, idx_bits: int = 64):
+        q = f32(q)
+        nq = q.size(0)
+        idx = torch.empty((nq, k), dtype=torch.int64 if idx_bits == 64 else torch.int32, device=q.device)
+        d2 = torch.empty((nq, k), dtype=torch.float32, device=q.device) if with_d2 else None
+        check(lib().pcd_knn(self.handle, ptr(q), nq, int(k), ptr(idx), idx_bits, 0, int(exclude_self), ptr(d2),
+                            c_void_p(stream_ptr())), "pcd_knn")
+        return (idx, d2) if with_d2 else idx
+
+    def nn(self, q: torch.Tensor):
+        q = f32(q)
+        d2 = torch.empty(q.size(0), dtype=torch.float32, device=q.device)
+        idx = torch.empty(q.size(0), dtype=torch.int64, device=q.device)
+        check(lib().pcd_nn_dist(self.handle, ptr(q), q.size(0), ptr(d2), ptr(idx), c_void_p(stream_ptr())),
+              "pcd_nn_dist")
+        return d2, idx
+
+
+class FusedDenoiser:
+    """Persistent buffers of the fused loop (pcd_denoiser) bound to one Grid."""
+
+    def __init__(self, grid: Grid, k_max: int):
+        self.grid = grid
+        h = c_void_p()
+        check(lib().pcd_denoiser_create(grid.handle, int(k_max), ctypes.byref(h)), "pcd_denoiser_create")
+        self.handle = h
+        self.k_max = k_max
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.pcd_denoiser_destroy(h)
+            self.handle = None
+
+    def load(self, pos: torch.Tensor, n: torch.Tensor):
+        pos, n = f32(pos), f32(n)
+        check(lib().pcd_denoiser_load(self.handle, ptr(pos), ptr(n), c_void_p(stream_ptr())), "pcd_denoiser_load")
+
+    def iterate(self, params: DenoiseParams, iterations: int):
+        check(lib().pcd_denoiser_iterate(self.handle, ctypes.byref(params), int(iterations), c_void_p(stream_ptr())),
+              "pcd_denoiser_iterate")
+
+    def store(self, pos=None, n=None, classes=None, edge_vectors=None):
+        check(lib().pcd_denoiser_store(self.handle, ptr(pos), ptr(n), ptr(classes), ptr(edge_vectors),
+                                       c_void_p(stream_ptr())), "pcd_denoiser_store")
+
+    def set_timing(self, on: bool):
+        check(lib().pcd_denoiser_set_timing(self.handle, int(on)), "pcd_denoiser_set_timing")
+
+    def timing(self):
+        buf = (c_float * 8)()
+        nw = c_int(0)
+        check(lib().pcd_denoiser_get_timing(self.handle, buf, 8, ctypes.byref(nw)), "pcd_denoiser_get_timing")
+        return [buf[i] for i in range(nw.value)]
+
+
+def make_params(k=16, k_update=8, rho=None, tau=0.3, damp=3.0, class_scale=0.2, d=1.0,
+                phases=((0, STEP_FLAT, 1.0), (1, STEP_EDGE, 0.2), (2, STEP_FEATURE, 1.0))) -> DenoiseParams:
+    import math
+    p = DenoiseParams()
+    p.k, p.k_update = int(k), int(k_update)
+    p.rho = float(math.pi * 5 / 12 if rho is None else rho)
+    p.tau, p.damp, p.class_scale, p.d = float(tau), float(damp), float(class_scale), float(d)
+    p.nphases = len(phases)
+    for t, (c, kind, a) in enumerate(phases):
+        p.phase_class[t], p.phase_kind[t], p.phase_alpha[t] = int(c), int(kind), float(a)
+    return p
+
+
+# ----------------------------------------------------------------------------------------------- op wrappers
+def nvt_csr(pos, n, ci, off, nbr, rho):
+    m = ci.size(0)
+    ev = torch.empty((m, 3), dtype=torch.float32, device=pos.device)
+    evec = torch.empty((m, 3, 3), dtype=torch.float32, device=pos.device)
+    check(lib().pcd_nvt_csr(ptr(pos), ptr(n), pos.size(0), ptr(ci), ptr(off), ptr(nbr), m, float(rho), ptr(ev),
+                            ptr(evec), c_void_p(stream_ptr())), "pcd_nvt_csr")
+    return ev, evec
+
+
+def vu_smooth(eigval, eigvec, n, tau, damp):
+    out = torch.empty_like(n)
+    check(lib().pcd_vu_smooth(ptr(eigval), ptr(eigvec), ptr(n), n.size(0), float(tau), float(damp), ptr(out),
+                              c_void_p(stream_ptr())), "pcd_vu_smooth")
+    return out
+
+
+def classify(eigval, scale, want_features=False):
+    m = eigval.size(0)
+    cls = torch.empty(m, dtype=torch.int64, device=eigval.device)
+    feat = torch.empty((m, 3), dtype=torch.float32, device=eigval.device) if want_features else None
+    check(lib().pcd_classify(ptr(eigval), m, float(scale), ptr(feat), ptr(cls), c_void_p(stream_ptr())),
+          "pcd_classify")
+    return cls, feat
+
+
+def pca_dense(pos, nbr, k):
+    n = pos.size(0)
+    ev = torch.empty((n, 3), dtype=torch.float32, device=pos.device)
+    evec = torch.empty((n, 3, 3), dtype=torch.float32, device=pos.device)
+    check(lib().pcd_pca_dense(ptr(pos), n, ptr(nbr), int(k), ptr(ev), ptr(evec), c_void_p(stream_ptr())),
+          "pcd_pca_dense")
+    return ev, evec
+
+
+def step_csr(kind, pos, n, edge_vectors, ci, off, nbr, d, alpha):
+    m = ci.size(0)
+    out = torch.empty((m, 3), dtype=torch.float32, device=pos.device)
+    check(lib().pcd_step_csr(int(kind), ptr(pos), ptr(n), ptr(edge_vectors), pos.size(0), ptr(ci), ptr(off),
+                             ptr(nbr), m, float(d), float(alpha), ptr(out), c_void_p(stream_ptr())), "pcd_step_csr")
+    return out
+
+
+def edge_length_sum(pos, a, b):
+    s = torch.empty(1, dtype=torch.float64, device=pos.device)
+    check(lib().pcd_edge_length_sum(ptr(pos), ptr(a), ptr(b), a.size(0), ptr(s), c_void_p(stream_ptr())),
+          "pcd_edge_length_sum")
+    return s
+
+
+def mesh_update(v, f, fn, vf, ni, k):
+    check(lib().pcd_mesh_update(ptr(v), v.size(0), ptr(f), ptr(fn), f.size(0), ptr(vf), ptr(ni), int(k),
+                                c_void_p(stream_ptr())), "pcd_mesh_update")
+
+
+def host_eigh3(t6):
+    """CPU build of the kernels' eigen-decomposition: t6 (m, 6) float32 -> (w (m,3), v (m,3,3))."""
+    import numpy as np
+    t6 = np.ascontiguousarray(t6, dtype=np.float32)
+    m = t6.shape[0]
+    w = np.empty((m, 3), np.float32)
+    v = np.empty((m, 3, 3), np.float32)
+    check(lib().pcd_host_eigh3(t6.ctypes.data, m, w.ctypes.data, v.ctypes.data), "pcd_host_eigh3")
+    return w, v
+
+
+def host_vu_smooth(w, v, n, tau=0.3, damp=3.0):
+    import numpy as np
+    w = np.ascontiguousarray(w, np.float32); v = np.ascontiguousarray(v, np.float32)
+    n = np.ascontiguousarray(n, np.float32)
+    out = np.empty_like(n)
+    check(lib().pcd_host_vu_smooth(w.ctypes.data, v.ctypes.data, n.ctypes.data, n.shape[0], float(tau), float(damp),
+                                   out.ctypes.data), "pcd_host_vu_smooth")
+    return out
+
+
+def host_solve3(a, b):
+    import numpy as np
+    a = np.ascontiguousarray(a, np.float32); b = np.ascontiguousarray(b, np.float32)
+    x = np.zeros_like(b)
+    ok = np.zeros(b.shape[0], np.int32)
+    check(lib().pcd_host_solve3(a.ctypes.data, b.ctypes.data, b.shape[0], x.ctypes.data, ok.ctypes.data),
+          "pcd_host_solve3")
+    return x, ok.astype(bool)
+
+
+def orient_normals_mst(pos_host, n_host, a_host, b_host):
+    """Host (CPU) MST orientation; tensors must be contiguous CPU f32 / int64.  Modifies n_host in place."""
+    assert not pos_host.is_cuda and not n_host.is_cuda
+    check(lib().pcd_orient_normals_mst(ptr(pos_host), ptr(n_host), pos_host.size(0), ptr(a_host), ptr(b_host),
+                                       a_host.size(0)), "pcd_orient_normals_mst")

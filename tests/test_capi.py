@@ -1,0 +1,144 @@
+"""CPU checks of the C-ABI boundary (include/pcd.h <-> libpcd.so <-> pcd_native), no GPU compute.
+
+* the library loads and exports every entry point the header declares; pcd_native binds exactly those
+* argument validation fails with PCD_ERR_ARG + pcd_last_error() before touching a device
+* the host builds of the kernels' per-point math (pcd_host_*) agree with the reference's own libraries:
+  eigen-decomposition vs MKL torch.linalg.eigh (values AND eigenvector signs), VU smoothing and 3x3 solves vs the
+  oracle, MST orientation (host C++) vs the oracle.
+"""
+import ctypes
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import pcd_native as nat
+from oracle import pcd_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pcd.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(pcd_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = nat.lib()
+    syms = header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(L, s), f"libpcd.so does not export {s}"
+
+
+def test_binding_covers_header_exactly():
+    assert sorted(nat.exported_symbols()) == header_symbols()
+
+
+def test_version_and_limits():
+    L = nat.lib()
+    assert L.pcd_version() >= 1
+    assert L.pcd_max_k() == 64
+
+
+def test_argument_errors_are_reported():
+    L = nat.lib()
+    idx = ctypes.c_void_p()
+    rc = L.pcd_knn(None, None, 10, 8, None, 64, 0, 0, None, None)
+    assert rc == nat.PCD_ERR_ARG
+    assert b"grid is null" in L.pcd_last_error()
+    rc = L.pcd_grid_build(None, 0, 16, 0.0, None, ctypes.byref(idx))
+    assert rc == nat.PCD_ERR_ARG and not idx.value
+    with pytest.raises(ValueError):
+        nat.check(L.pcd_step_csr(99, None, None, None, 0, None, None, None, 0, 1.0, 1.0, None, None), "step")
+    with pytest.raises(ValueError):
+        nat.check(L.pcd_denoiser_create(None, 16, ctypes.byref(idx)), "create")
+
+
+def _nvt_tensors(golden):
+    f = golden("fandisk_k32")
+    pos, n, idx = f["pos0"], f["n0"], f["knn32"]
+    vj, nj = pos[idx], n[idx]
+    dv = vj - pos[:, None]
+    dn = dv / np.maximum(np.linalg.norm(dv, axis=-1, keepdims=True), 1e-12)
+    w = (np.arccos(np.abs(np.clip((dn * nj).sum(-1), -1, 1))) > np.float32(math.pi * 5 / 12)).astype(np.float32)
+    w[w.sum(1) == 0] = 1
+    T = (w[..., None, None] * nj[..., :, None] * nj[..., None, :]).sum(1) / w.sum(1)[:, None, None]
+    return T.astype(np.float32)
+
+
+def _t6(T):
+    return np.stack([T[:, 0, 0], T[:, 1, 0], T[:, 2, 0], T[:, 1, 1], T[:, 2, 1], T[:, 2, 2]], 1)
+
+
+@pytest.mark.parametrize("which", ["nvt", "random", "pca", "degenerate"])
+def test_host_eigh_matches_torch(golden, which):
+    rng = np.random.default_rng(1)
+    if which == "nvt":
+        T = _nvt_tensors(golden)
+    elif which == "random":
+        R = rng.standard_normal((4000, 3, 3)).astype(np.float32)
+        T = ((R + R.transpose(0, 2, 1)) / 2).astype(np.float32)
+    elif which == "pca":
+        s = golden("steps")
+        vj = s["pos"][s["knn12_noself"]]
+        d = vj - vj.mean(1, keepdims=True)
+        T = (d[..., :, None] * d[..., None, :]).sum(1).astype(np.float32)
+    else:  # exact outer products of axis-aligned / lattice-like normals (repeated eigenvalues)
+        nrm = np.eye(3, dtype=np.float32)[rng.integers(0, 3, (500, 4))]
+        T = (nrm[..., :, None] * nrm[..., None, :]).mean(1).astype(np.float32)
+    w, v = nat.host_eigh3(_t6(T))
+    tw, tv = torch.linalg.eigh(torch.from_numpy(T))
+    tw, tv = tw.numpy(), tv.numpy()
+    scale = np.abs(tw).max(1, keepdims=True) + 1e-30
+    assert np.abs(w - tw).max() <= 1e-5 * scale.max() + 1e-12
+    # eigenvector signs: MKL's wherever the eigenvalue is simple.  A handful of matrices sit on a sign decision of
+    # the QL sweep (slartg's |f| > |g| test within rounding) and may flip; they are < 0.1 %.
+    gap = np.minimum(np.abs(np.diff(tw, axis=1, prepend=-np.inf)), np.abs(np.diff(tw, axis=1, append=np.inf)))
+    simple = gap > 1e-4 * scale
+    dots = (v * tv).sum(1)
+    assert (dots[simple] > 0.999).mean() >= 0.999, f"{which}: sign or vector mismatch on simple eigenvalues"
+
+
+def test_host_vu_smooth_matches_oracle(golden):
+    s = golden("steps")
+    for rho in ("a5pi12", "api3"):
+        ev, evec, n1 = s[f"nvt_{rho}_k16_eigval"], s[f"nvt_{rho}_k16_eigvec"], s["n1"]
+        out = nat.host_vu_smooth(ev, evec, n1)
+        ref = s[f"nvt_{rho}_k16_vu"]           # the reference's own output
+        err = np.linalg.norm(out - ref, axis=1)
+        assert np.percentile(err, 99.9) < 1e-6 and err.max() < 1e-5
+
+
+def test_host_solve3():
+    rng = np.random.default_rng(3)
+    A = rng.standard_normal((2000, 3, 3)).astype(np.float32)
+    b = rng.standard_normal((2000, 3)).astype(np.float32)
+    A[:10, 2] = 0.0                              # exactly singular rows
+    A[10:20, :, 0] = 0.0                         # exactly singular column
+    x, ok = nat.host_solve3(A, b)
+    _, ok_ref = O.inv_ex(A)
+    assert (ok == ok_ref).all()
+    good = ok & (np.linalg.cond(A.astype(np.float64)) < 1e3)
+    xr = np.linalg.solve(A[good].astype(np.float64), b[good].astype(np.float64)[..., None])[..., 0]
+    np.testing.assert_allclose(x[good], xr, rtol=1e-4, atol=1e-4)
+
+
+def test_orientation_host_matches_oracle(golden):
+    lat = golden("lattice")
+    pos = lat["n17_j1_pos"]
+    nbr = O.knn_graph_noself(pos, 12)
+    n0 = O.pca_normals_unoriented(pos, nbr).astype(np.float32)
+    ref = O.orient_normals_mst(pos, n0.copy(), nbr)
+    n = torch.from_numpy(n0.copy())
+    a = torch.from_numpy(np.repeat(np.arange(len(pos)), 12))
+    b = torch.from_numpy(nbr.reshape(-1).copy())
+    nat.orient_normals_mst(torch.from_numpy(pos.copy()), n, a, b)
+    assert ((n.numpy() * ref).sum(1) > 0.999).mean() > 0.995
+    # and with the reference's own oriented normals
+    assert (np.sign((n.numpy() * lat["n17_j1_n"]).sum(1)) > 0).mean() > 0.99

@@ -1,0 +1,387 @@
+"""GPU parity: the HIP path (through libpcd's C-ABI and the drop-in classes) against the reference's golden vectors
+and the CPU oracle.  Run on an MI355X with `pytest -m gpu`.
+
+Tolerances (fp32): kNN sets identical except distance near-ties; eigenvalues <= 2e-6 abs;
+smoothed normals <= 1e-4 rad except near a threshold; classes identical except near-margin points (>= 99.8 %);
+positions p99 <= 1e-5 x bbox for one step; multi-iteration runs within the reference's own fp32-vs-fp64 envelope.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import pcd_native as nat
+from oracle import pcd_oracle as O
+from Pointcloud.Modules.Decompositionor import Decompositionor
+from Pointcloud.Modules.Denoiser import Denoiser
+from Pointcloud.Modules.Object import Pointcloud
+from Pointcloud.Modules.Processor import Processor
+from Pointcloud.Modules.Selector import Selection, Selector
+from Pointcloud.Modules.Utils import TorchUtils
+from PatchGeneration.Modules.Mesh import Mesh
+
+pytestmark = pytest.mark.gpu
+ANGLE = math.pi * 5 / 12
+
+
+def angle(a, b):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    a = a / np.linalg.norm(a, axis=-1, keepdims=True)
+    b = b / np.linalg.norm(b, axis=-1, keepdims=True)
+    s = np.sign((a * b).sum(-1, keepdims=True)); s[s == 0] = 1
+    return 2 * np.arcsin(np.clip(np.linalg.norm(a - s * b, axis=-1) / 2, 0, 1))
+
+
+def T(x, dev):
+    return torch.as_tensor(np.ascontiguousarray(x)).to(dev)
+
+
+def knn_rows_agree(got, ref, dist_sorted):
+    """Fraction of rows whose neighbour SET matches, counting rows with a boundary near-tie as matching."""
+    k = got.shape[1]
+    same = np.array([set(a) == set(b) for a, b in zip(got, ref)])
+    if dist_sorted is not None and dist_sorted.shape[1] > k:
+        dk, dk1 = dist_sorted[:, k - 1], dist_sorted[:, k]
+        tie = (dk1 - dk) <= 1e-6 * np.maximum(dk1, 1e-30)
+        same |= tie
+    return same.mean()
+
+
+@pytest.fixture(scope="module")
+def fan(golden):
+    return golden("fandisk_k32")
+
+
+@pytest.fixture(scope="module")
+def steps(golden):
+    return golden("steps")
+
+
+# --------------------------------------------------------------------------------------------------- kNN (H1, H2)
+def test_knn_frozen_snapshot(fan, gpu):
+    pos = T(fan["pos0"], gpu)
+    grid = nat.Grid(pos, k_hint=32)
+    idx, d2 = grid.knn(pos, 32, with_d2=True)
+    idx, d2 = idx.cpu().numpy(), d2.cpu().numpy()
+    _, dref = O.FrozenKNN(fan["pos0"]).query(fan["pos0"], 33)
+    assert knn_rows_agree(idx, fan["knn32"], dref) >= 0.9999
+    assert (idx == fan["knn32"]).mean() > 0.999            # order too, except exact/near ties
+    np.testing.assert_allclose(np.sqrt(d2), fan["knn32_d"], rtol=1e-5, atol=1e-6)
+    assert (np.diff(d2, axis=1) >= 0).all()                   # ascending
+
+
+@pytest.mark.parametrize("k", [1, 6, 8, 16, 24, 32, 48, 64])
+def test_knn_moving_queries_all_k(fan, gpu, k):
+    """Queries are the CURRENT (moved) positions, candidates the frozen snapshot (Selector.py:141,243)."""
+    rng = np.random.default_rng(k)
+    snap = fan["pos0"]
+    q = (snap + rng.normal(0, 0.02, snap.shape)).astype(np.float32)
+    q[:50] += rng.normal(0, 2.0, (50, 3)).astype(np.float32)   # some far-moved queries (shell expansion)
+    grid = nat.Grid(T(snap, gpu), k_hint=16)
+    idx = grid.knn(T(q, gpu), k).cpu().numpy()
+    ref, dref = O.FrozenKNN(snap).query(q, min(k + 1, len(snap)))
+    assert knn_rows_agree(idx, ref[:, :k], dref) >= 0.9995
+
+
+def test_knn_outlier_query_exhaustive(fan, gpu):
+    snap = fan["pos0"]
+    q = np.array([[1e4, -3e4, 7e3], [0.0, 0.0, 0.0]], np.float32)
+    grid = nat.Grid(T(snap, gpu))
+    idx = grid.knn(T(q, gpu), 8).cpu().numpy()
+    ref, _ = O.FrozenKNN(snap).query(q, 8)
+    assert all(set(a) == set(b) for a, b in zip(idx, ref))
+
+
+def test_knn_graph_excludes_self(steps, gpu):
+    from Pointcloud.Modules.GraphBuilder import GraphBuilder
+    pc = Pointcloud(T(steps["pos"], gpu))
+    ei = GraphBuilder(pc).getKNNEdgeIndex(12).cpu().numpy()
+    nbr = ei[1].reshape(-1, 12)
+    assert (ei[0] == np.repeat(np.arange(len(steps["pos"])), 12)).all()
+    assert not (nbr == np.arange(len(nbr))[:, None]).any()
+    assert (np.sort(nbr, 1) == np.sort(steps["knn12_noself"], 1)).all(1).mean() > 0.999
+
+
+def test_knn_duplicates_and_ties(gpu):
+    """Exact duplicates and lattice ties: order by (d², index), sets exact."""
+    g = np.stack(np.meshgrid(*[np.arange(6, dtype=np.float32)] * 3, indexing="ij"), -1).reshape(-1, 3)
+    pts = np.concatenate([g, g[:20]])                       # 20 exact duplicates
+    grid = nat.Grid(T(pts, gpu), k_hint=8)
+    idx, d2 = grid.knn(T(pts, gpu), 7, with_d2=True)
+    idx, d2 = idx.cpu().numpy(), d2.cpu().numpy()
+    dd = ((pts[:, None] - pts[None]) ** 2).sum(-1)
+    for r in range(len(pts)):
+        order = np.lexsort((np.arange(len(pts)), dd[r]))[:7]
+        assert list(idx[r]) == list(order), r
+
+
+def test_knn_rejects_k_larger_than_n(gpu):
+    grid = nat.Grid(torch.rand(5, 3, device=gpu))
+    with pytest.raises(ValueError):
+        grid.knn(torch.rand(3, 3, device=gpu), 6)
+
+
+def test_selector_api(fan, gpu):
+    pos = T(fan["pos0"], gpu)
+    g = Processor(Pointcloud(pos.clone())).graph
+    sel = Selector(g).getKNNSelection(8)
+    assert sel.j.dtype == torch.int64 and sel.j.device == pos.device
+    assert (sel.slices.cpu().numpy() == np.arange(len(pos) + 1) * 8).all()
+    sub = torch.tensor([5, 3, 100], device=gpu)
+    f = sel.filter(sub)
+    assert (f.j.view(3, 8).cpu().numpy() == sel.j.view(-1, 8)[sub].cpu().numpy()).all()
+    ei = sel.getEdgeIndex()
+    assert ei.shape == (2, len(pos) * 8)
+
+
+# --------------------------------------------------------------------------------------------------- NVT (H5-H7)
+@pytest.mark.parametrize("rho", ["a5pi12", "api3"])
+@pytest.mark.parametrize("k", [8, 16])
+def test_nvt_decomposition(steps, gpu, rho, k):
+    pos, n1 = T(steps["pos"], gpu), T(steps["n1"], gpu)
+    pc = Pointcloud(pos.clone())
+    g = Processor(pc).graph
+    knn = torch.as_tensor(steps[f"knn{k}"].astype(np.int64)).to(gpu)
+    m = knn.size(0)
+    sel = Selection(torch.arange(m, device=gpu), knn.reshape(-1), torch.arange(m + 1, device=gpu) * k)
+    r = ANGLE if rho == "a5pi12" else math.pi / 3
+    dec = Decompositionor(g).getBetterFilteredNVT(sel, n1, r)
+    ev = dec.eigval.cpu().numpy()
+    np.testing.assert_allclose(ev, steps[f"nvt_{rho}_k{k}_eigval"], atol=2e-6)
+    cls = dec.getClasses().cpu().numpy()
+    assert (cls == steps[f"nvt_{rho}_k{k}_classes"]).mean() >= 0.999
+    vu = dec.getVUSmoothedNormals(n1).cpu().numpy()
+    a = angle(vu, steps[f"nvt_{rho}_k{k}_vu"])
+    assert np.percentile(a, 99.5) < 1e-4 and (a < 1e-2).mean() > 0.998
+    pl, li, sp = dec.getNVTFeatures()
+    feats = torch.stack([pl, li, sp], 1).cpu().numpy()
+    np.testing.assert_allclose(feats, steps[f"nvt_{rho}_k{k}_features"], rtol=1e-4, atol=2e-5)
+
+
+# --------------------------------------------------------------------------------------------------- steps (H9-H12)
+@pytest.mark.parametrize("alpha", [1.0, 0.2])
+@pytest.mark.parametrize("kind", ["flat", "edge", "feature", "corner", "new", "dummy"])
+def test_denoiser_steps(steps, gpu, kind, alpha):
+    pos, n1 = T(steps["pos"], gpu), T(steps["n1"], gpu)
+    g = Processor(Pointcloud(pos.clone())).graph
+    den = Denoiser(g)
+    sub = torch.as_tensor(steps["subset"]).to(gpu)
+    knn = torch.as_tensor(steps["knn8"].astype(np.int64)).to(gpu)
+    full = Selection(torch.arange(knn.size(0), device=gpu), knn.reshape(-1), torch.arange(knn.size(0) + 1, device=gpu) * 8)
+    s = full.filter(sub)
+    ev = T(steps["edge_vectors"], gpu)
+    d = float(steps["d"])
+    bbox = np.linalg.norm(steps["pos"].max(0) - steps["pos"].min(0))
+    for dd, suffix in ((d, ""), (1e9, "_noclamp")):
+        key = f"{kind}_a{alpha}{suffix}"
+        if key not in steps:
+            continue
+        if kind == "edge":
+            out = den.edge_step(s, n1, ev, dd, alpha)
+        else:
+            out = getattr(den, f"{kind}_step")(s, n1, dd, alpha)
+        dev = np.linalg.norm(out.cpu().numpy() - steps[key], axis=1) / bbox
+        assert np.percentile(dev, 95) < 1e-5, (key, np.percentile(dev, 95))
+        assert (dev < 1e-3).mean() > 0.99, key
+
+
+def test_steps_on_filtered_csr_selection(steps, gpu):
+    """Ragged CSR selection (non-uniform segment lengths), compared with the oracle on the same rows."""
+    pos, n1 = steps["pos"], steps["n1"]
+    rng = np.random.default_rng(5)
+    lens = rng.integers(3, 9, 500)
+    ci = rng.choice(len(pos), 500, replace=False)
+    rows = [steps["knn8"][c][:l] for c, l in zip(ci, lens)]
+    off = np.concatenate([[0], np.cumsum(lens)])
+    out = nat.step_csr(nat.STEP_FEATURE, T(pos, gpu), T(n1, gpu), None, T(ci.astype(np.int64), gpu),
+                       T(off.astype(np.int64), gpu), T(np.concatenate(rows).astype(np.int64), gpu), 1e9, 1.0)
+    ref = np.stack([O.feature_step(pos, n1, np.array([c]), r[None], 1e9, 1.0)[0] for c, r in zip(ci, rows)])
+    dev = np.linalg.norm(out.cpu().numpy() - ref, axis=1)
+    assert np.percentile(dev, 95) < 1e-5
+
+
+# --------------------------------------------------------------------------------------------------- PCA normals (H15)
+def test_pca_normals_and_orientation(steps, golden, gpu):
+    from Pointcloud.Modules.GraphBuilder import GraphBuilder
+    pos = T(steps["pos"], gpu)
+    gb = GraphBuilder(Pointcloud(pos.clone()))
+    ei = torch.stack([torch.arange(len(pos), device=gpu).repeat_interleave(12),
+                      T(steps["knn12_noself"].astype(np.int64), gpu).reshape(-1)])
+    ev = gb.getPVTDecompositionWithKNN(ei)[..., 0].cpu().numpy()
+    ref = steps["pca_n"]
+    dots = (ev * ref).sum(1) / np.linalg.norm(ev, axis=1) / np.linalg.norm(ref, axis=1)
+    assert (np.abs(dots) > 0.9999).mean() > 0.999
+    assert (dots > 0).mean() > 0.995                          # LAPACK sign convention reproduced
+    # full setAndFlipNormals on the fandisk input reproduces the reference's oriented normals
+    fan = golden("fandisk_k32")
+    gb2 = GraphBuilder(Pointcloud(T(fan["pos0"], gpu)))
+    gb2.graph.edge_index = gb2.getKNNEdgeIndex(12)
+    gb2.setAndFlipNormals(flip=True)
+    agree = (gb2.graph.n.cpu().numpy() * fan["n0"]).sum(1)
+    assert (agree > 0.999).mean() > 0.99
+
+
+# --------------------------------------------------------------------------------------------------- fused loop (H8, H13)
+def _fused(fan, gpu, iterations, k=32, k_u=8):
+    pc = Pointcloud(T(fan["pos0"], gpu).clone(), T(fan["n0"], gpu).clone())
+    proc = Processor(pc, k_hint=k)
+    fused = proc._fused_for(max(k, k_u))
+    fused.load(proc.graph.pos, proc.graph.n)
+    params = nat.make_params(k=k, k_update=k_u, d=float(fan["d"]))
+    fused.iterate(params, iterations)
+    N = len(fan["pos0"])
+    pos = torch.empty((N, 3), device=gpu); n = torch.empty((N, 3), device=gpu)
+    cls = torch.empty(N, dtype=torch.int64, device=gpu)
+    fused.store(pos, n, cls)
+    return pos.cpu().numpy(), n.cpu().numpy(), cls.cpu().numpy()
+
+
+def test_fused_iteration_matches_reference(fan, gpu):
+    pos, n, cls = _fused(fan, gpu, 1)
+    assert (cls == fan["it1_classes"]).mean() >= 0.998
+    a = angle(n, fan["it1_f_n"])
+    assert np.percentile(a, 99) < 1e-4 and (a < 1e-2).mean() > 0.998
+    bbox = np.linalg.norm(fan["pos0"].max(0) - fan["pos0"].min(0))
+    dev = np.linalg.norm(pos - fan["it1_pos_after_2"], axis=1) / bbox
+    assert np.percentile(dev, 99) < 3e-4 and np.median(dev) < 1e-6
+
+
+def test_fused_ten_iterations_cd_envelope(fan, gpu):
+    """Chaotic after a few iterations: compare Chamfer trajectories within the fp32-vs-fp64 spread."""
+    gt = fan["gt"]
+    pc = Pointcloud(T(fan["pos0"], gpu).clone(), T(fan["n0"], gpu).clone())
+    proc = Processor(pc, k_hint=32)
+    cds = [float(TorchUtils.ChamferDistance(T(gt, gpu), proc.graph.pos).mean())]
+    for _ in range(10):
+        proc.denoise(iterations=1, k=32, k_update=8, d=float(fan["d"]))
+        cds.append(float(TorchUtils.ChamferDistance(T(gt, gpu), proc.graph.pos).mean()))
+    ref32, ref64 = fan["cd_f32"], fan["cd_f64"]
+    env = np.maximum(np.abs(ref32 - ref64), 0.02 * ref32)
+    assert np.all(np.abs(np.asarray(cds) - ref32) <= 2 * env + 1e-6), (cds, list(ref32))
+    assert abs(cds[1] - ref32[1]) / ref32[1] < 2e-3
+
+
+def test_processor_denoise_verbatim(golden, gpu):
+    """Processor.denoise() with its defaults (k=16, k_u=8, 2 iterations, d=2l), aliasing included."""
+    g = golden("fandisk_denoise")
+    v = T(g["pos0"], gpu).clone()
+    pc = Pointcloud(v, T(g["n0"], gpu).clone())
+    proc = Processor(pc)
+    proc.denoise()
+    assert proc.graph.pos is v and pc.v is v                 # graph.pos mutated in place (GraphBuilder.py:50)
+    bbox = np.linalg.norm(g["pos0"].max(0) - g["pos0"].min(0))
+    dev = np.linalg.norm(v.cpu().numpy() - g["pos"], axis=1) / bbox
+    assert np.percentile(dev, 99) < 5e-3 and np.median(dev) < 1e-5
+    a = angle(proc.graph.n.cpu().numpy(), g["n"])
+    assert np.median(a) < 1e-5
+
+
+def test_processor_on_cpu_tensors_returns_cpu(golden, gpu):
+    g = golden("fandisk_denoise")
+    v = torch.from_numpy(g["pos0"].copy())
+    pc = Pointcloud(v, torch.from_numpy(g["n0"].copy()))
+    proc = Processor(pc)
+    proc.denoise()
+    assert v.device.type == "cpu" and proc.graph.n.device.type == "cpu"
+    bbox = np.linalg.norm(g["pos0"].max(0) - g["pos0"].min(0))
+    dev = np.linalg.norm(v.numpy() - g["pos"], axis=1) / bbox
+    assert np.median(dev) < 1e-5
+
+
+def test_get_my_feature_decomposition(fan, gpu):
+    pc = Pointcloud(T(fan["pos0"], gpu).clone(), T(fan["n0"], gpu).clone())
+    dec, f_n = Processor(pc).getMyFeatureDecomposition(32)
+    assert (dec.getClasses().cpu().numpy() == fan["it1_classes"]).mean() >= 0.998
+    np.testing.assert_allclose(dec.eigval.cpu().numpy(), fan["it1_eigval2"], atol=1e-5)
+
+
+def test_denoise_until_minimum_error(fan, gpu):
+    pc = Pointcloud(T(fan["pos0"], gpu).clone(), T(fan["n0"], gpu).clone())
+    proc = Processor(pc)
+    den = proc.denoiser
+    strategy = {0: den.flat_step, 1: den.edge_step, 2: den.feature_step}
+    l = float(proc.meanEdgeLength())
+    pos, err, its = proc.denoiseUntilMinimumError(T(fan["gt"], gpu), strategy, k=8, alpha=[1, 0.2, 1], d=2 * l)
+    assert its >= 0 and pos.shape == (len(fan["pos0"]), 3)
+    assert torch.equal(proc.graph.pos.cpu(), torch.from_numpy(fan["pos0"]))   # restored noisy state
+    e0 = float(TorchUtils.PaperDistance(T(fan["gt"], gpu), T(fan["pos0"], gpu)).mean())
+    assert float(err[0].mean()) <= e0 + 1e-9
+
+
+# --------------------------------------------------------------------------------------------------- KAT + edge cases
+def test_lattice_cube_known_answer(golden, gpu):
+    lat = golden("lattice")
+    for tag in ("n9_j1", "n17_j1", "n9_j0", "n17_j0"):
+        pc = Pointcloud(T(lat[f"{tag}_pos"], gpu).clone(), T(lat[f"{tag}_n"], gpu).clone())
+        dec, _ = Processor(pc).getMyFeatureDecomposition()
+        cls = dec.getClasses().cpu().numpy()
+        acc = (cls == lat[f"{tag}_gt"]).mean()
+        assert acc >= float(lat[f"{tag}_acc"]) - 0.01, (tag, acc)
+        if tag.endswith("j1"):
+            assert (cls == lat[f"{tag}_classes"]).mean() > 0.995
+
+
+def test_flat_plane_is_a_fixed_point(gpu):
+    """A noiseless plane with exact normals: every point flat, zero displacement (idempotence)."""
+    xs = np.stack(np.meshgrid(np.linspace(0, 1, 60), np.linspace(0, 1, 60), indexing="ij"), -1).reshape(-1, 2)
+    pos = np.concatenate([xs, np.zeros((len(xs), 1))], 1).astype(np.float32)
+    nrm = np.tile(np.array([[0, 0, 1]], np.float32), (len(pos), 1))
+    pc = Pointcloud(T(pos, gpu), T(nrm, gpu))
+    proc = Processor(pc)
+    proc.denoise(iterations=3)
+    assert np.abs(pc.v.cpu().numpy() - pos).max() < 1e-6
+
+
+def test_fused_zero_phases_only_updates_normals(fan, gpu):
+    pc = Pointcloud(T(fan["pos0"], gpu).clone(), T(fan["n0"], gpu).clone())
+    proc = Processor(pc, k_hint=16)
+    proc._run_fused(1, 16, 8, 1.0, phases=())
+    np.testing.assert_array_equal(pc.v.cpu().numpy(), fan["pos0"])
+
+
+# --------------------------------------------------------------------------------------------------- mesh + metrics
+def test_mesh_update_vertex_updating(golden, gpu):
+    m = golden("mesh_update")
+    for k, key in ((1, "v_k1"), (15, "v_k15")):
+        mesh = Mesh(m["v"].copy(), m["f"].astype(np.int64))
+        mesh.updateVertices(m["n"], k=k)
+        np.testing.assert_allclose(mesh.v, m[key], rtol=0, atol=1e-10)
+
+
+def test_mesh_update_isolated_vertex_is_nan(gpu):
+    v = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [5, 5, 5]], np.float64)
+    f = np.array([[0, 1, 2]])
+    mesh = Mesh(v.copy(), f)
+    mesh.updateVertices(np.array([[0, 0, 1.0]]), k=1)
+    assert np.isnan(mesh.v[3]).all() and np.isfinite(mesh.v[:3]).all()
+
+
+def test_metrics(golden, gpu):
+    m = golden("metrics")
+    a, b = T(m["a"], gpu), T(m["b"], gpu)
+    np.testing.assert_allclose(TorchUtils.ChamferDistance(a, b).cpu().numpy(), m["chamfer"], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(TorchUtils.PaperDistance(a, b).cpu().numpy(), m["paper"], rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(TorchUtils.HausdorffDistance(a, b).cpu().numpy(), m["hausdorff"], rtol=1e-5, atol=1e-7)
+    proc = Processor(Pointcloud(b.clone()))
+    l = float(proc.meanEdgeLength())
+    assert abs(l - float(m["avg_edge_len"])) < 1e-5 * float(m["avg_edge_len"])
+
+
+# --------------------------------------------------------------------------------------------------- full-size properties
+def test_large_cloud_knn_exact_vs_bruteforce(gpu):
+    """1M points: exact k-th distances for 1,024 sampled queries (brute force on the GPU with torch as checker)."""
+    g = torch.Generator(device=gpu).manual_seed(0)
+    N = 1_000_000
+    u = torch.rand((N, 2), generator=g, device=gpu)
+    pos = torch.stack([torch.cos(6.28 * u[:, 0]) * (1 + 0.3 * torch.cos(6.28 * u[:, 1])),
+                       torch.sin(6.28 * u[:, 0]) * (1 + 0.3 * torch.cos(6.28 * u[:, 1])),
+                       0.3 * torch.sin(6.28 * u[:, 1])], 1)
+    pos = pos + 0.002 * torch.randn(pos.shape, generator=g, device=gpu)
+    grid = nat.Grid(pos, k_hint=32)
+    q = pos[:1024] + 0.004 * torch.randn((1024, 3), generator=g, device=gpu)
+    idx, d2 = grid.knn(q, 32, with_d2=True)
+    bf = torch.cdist(q.double(), pos.double()) ** 2
+    kth = torch.topk(bf, 32, largest=False).values[:, -1].float()
+    np.testing.assert_allclose(d2[:, -1].cpu().numpy(), kth.cpu().numpy(), rtol=1e-4, atol=1e-9)
+    assert (idx >= 0).all() and (idx < N).all()

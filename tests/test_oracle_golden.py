@@ -1,0 +1,177 @@
+"""Pin the CPU oracle (oracle/pcd_oracle.py) against golden vectors produced by the REFERENCE itself
+(tests/golden/make_golden.py).  CPU only; these establish that the checker used by the GPU parity tests is right.
+
+Tolerances follow SURVEY.md §8(c): discrete decisions (kNN sets, w_ij thresholds, classes, clamps) must agree except
+on near-ties; continuous outputs agree to fp32 rounding.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import pcd_oracle as O
+
+
+def angle(a, b):
+    """Unsigned angle between line directions, accurate near 0 (float64 chord, not arccos of an fp32 dot)."""
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    a = a / np.linalg.norm(a, axis=-1, keepdims=True)
+    b = b / np.linalg.norm(b, axis=-1, keepdims=True)
+    s = np.sign((a * b).sum(-1, keepdims=True)); s[s == 0] = 1
+    return 2 * np.arcsin(np.clip(np.linalg.norm(a - s * b, axis=-1) / 2, 0, 1))
+
+
+@pytest.fixture(scope="module")
+def fan(golden):
+    return golden("fandisk_k32")
+
+
+def test_knn_frozen_snapshot_matches_reference(fan):
+    knn = O.FrozenKNN(fan["pos0"])
+    idx, d = knn.query(fan["pos0"], 32)
+    assert (idx == fan["knn32"]).mean() > 0.9999
+    np.testing.assert_allclose(d, fan["knn32_d"], rtol=0, atol=1e-12)
+
+
+def test_mean_edge_length_and_d(fan):
+    knn = O.FrozenKNN(fan["pos0"])
+    l = O.mean_edge_length(fan["pos0"], knn)
+    assert abs(l - float(fan["l"])) < 1e-6 * float(fan["l"])
+
+
+def test_nvt1_eigenvalues(fan):
+    ci = np.arange(len(fan["pos0"]))
+    w, v = O.better_filtered_nvt(fan["pos0"], fan["n0"], ci, fan["knn32"], math.pi * 5 / 12)
+    np.testing.assert_allclose(w, fan["eigval1"], atol=2e-6)
+
+
+def test_iteration1_stages(fan):
+    knn = O.FrozenKNN(fan["pos0"])
+    rec = {}
+    pos, f_n, cls = O.denoise_iteration(fan["pos0"], fan["n0"], knn, float(fan["d"]), 32, 8, record=rec)
+    assert (cls == fan["it1_classes"]).mean() >= 0.999
+    assert np.percentile(angle(f_n, fan["it1_f_n"]), 99.9) < 1e-4
+    np.testing.assert_allclose(rec["eigval2"], fan["it1_eigval2"], atol=2e-6)
+    bbox = np.linalg.norm(fan["pos0"].max(0) - fan["pos0"].min(0))
+    for key in range(3):
+        dev = np.linalg.norm(rec[f"pos_after_{key}"] - fan[f"it1_pos_after_{key}"], axis=1) / bbox
+        assert np.percentile(dev, 99) < 1e-5, (key, np.percentile(dev, 99))
+
+
+def test_ten_iterations_within_fp32_fp64_envelope(fan):
+    """End-to-end: the oracle's CD trajectory stays within the reference's own fp32-vs-fp64 spread."""
+    knn = O.FrozenKNN(fan["pos0"])
+    pos, n = fan["pos0"].copy(), fan["n0"].copy()
+    cds = [O.chamfer(fan["gt"], pos).mean()]
+    for _ in range(10):
+        pos, n, _ = O.denoise_iteration(pos, n, knn, float(fan["d"]), 32, 8)
+        cds.append(O.chamfer(fan["gt"], pos).mean())
+    ref32, ref64 = fan["cd_f32"], fan["cd_f64"]
+    env = np.maximum(np.abs(ref32 - ref64), 0.02 * ref32)
+    assert np.all(np.abs(np.asarray(cds) - ref32) <= 2 * env + 1e-6), (cds, ref32, ref64)
+    assert abs(cds[1] - ref32[1]) / ref32[1] < 1e-3
+
+
+def test_processor_denoise_verbatim(golden):
+    g = golden("fandisk_denoise")
+    pos, n = O.denoise(g["pos0"], g["n0"], iterations=2, k=16, k_update=8)
+    bbox = np.linalg.norm(g["pos0"].max(0) - g["pos0"].min(0))
+    dev = np.linalg.norm(pos - g["pos"], axis=1) / bbox
+    assert np.percentile(dev, 99) < 5e-3
+    assert np.median(dev) < 1e-5
+
+
+@pytest.fixture(scope="module")
+def steps(golden):
+    return golden("steps")
+
+
+@pytest.mark.parametrize("rho", ["a5pi12", "api3"])
+@pytest.mark.parametrize("k", [8, 16])
+def test_nvt_vu_classes(steps, rho, k):
+    pos, n1 = steps["pos"], steps["n1"]
+    ci = np.arange(len(pos))
+    r = math.pi * 5 / 12 if rho == "a5pi12" else math.pi / 3
+    w, v = O.better_filtered_nvt(pos, n1, ci, steps[f"knn{k}"], r)
+    np.testing.assert_allclose(w, steps[f"nvt_{rho}_k{k}_eigval"], atol=2e-6)
+    # smoothing and classification fed the reference's own decomposition
+    vu = O.vu_smoothed_normals(steps[f"nvt_{rho}_k{k}_eigval"], steps[f"nvt_{rho}_k{k}_eigvec"], n1)
+    assert np.percentile(angle(vu, steps[f"nvt_{rho}_k{k}_vu"]), 99.9) < 1e-5
+    cls = O.classes(steps[f"nvt_{rho}_k{k}_eigval"])
+    assert (cls == steps[f"nvt_{rho}_k{k}_classes"]).all()
+    feats = np.stack(O.nvt_features(steps[f"nvt_{rho}_k{k}_eigval"]), 1)
+    np.testing.assert_allclose(feats, steps[f"nvt_{rho}_k{k}_features"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("alpha", [1.0, 0.2])
+@pytest.mark.parametrize("kind", ["flat", "edge", "feature", "corner", "new"])
+def test_denoiser_steps(steps, kind, alpha):
+    pos, n1, sub = steps["pos"], steps["n1"], steps["subset"]
+    nbr = steps["knn8"][sub]
+    d = float(steps["d"])
+    tag = f"a{alpha}"
+    bbox = np.linalg.norm(pos.max(0) - pos.min(0))
+    for dd, suffix in ((d, ""), (1e9, "_noclamp")):
+        key = f"{kind}_{tag}{suffix}"
+        if key not in steps:
+            continue
+        if kind == "edge":
+            out = O.edge_step(pos, n1, steps["edge_vectors"], sub, nbr, dd, alpha)
+        else:
+            out = O.STEPS[kind](pos, n1, sub, nbr, dd, alpha)
+        dev = np.linalg.norm(out - steps[key], axis=1) / bbox
+        # ill-conditioned 3x3 solves amplify fp32 rounding: gate the bulk tightly, allow a small tail
+        assert np.percentile(dev, 95) < 1e-5, (key, np.percentile(dev, 95))
+        assert (dev < 1e-3).mean() > 0.99, key
+
+
+def test_dummy_step(steps):
+    sub = steps["subset"]
+    np.testing.assert_array_equal(steps["dummy_a1.0"], steps["pos"][sub])
+
+
+def test_pca_normals_up_to_sign(steps):
+    nbr = O.knn_graph_noself(steps["pos"], 12)
+    assert (np.sort(nbr, 1) == np.sort(steps["knn12_noself"], 1)).mean() > 0.999
+    n = O.pca_normals_unoriented(steps["pos"], steps["knn12_noself"])
+    assert np.percentile(angle(n, steps["pca_n"]), 99.9) < 1e-3
+
+
+def test_lattice_kat(golden):
+    lat = golden("lattice")
+    for tag in ("n9_j0", "n17_j0", "n9_j1", "n17_j1"):
+        pos, n = lat[f"{tag}_pos"], lat[f"{tag}_n"]
+        knn = O.FrozenKNN(pos)
+        (w2, _), f_n, _ = O.feature_decomposition(pos, n, knn, 16)
+        cls = O.classes(w2)
+        acc = (cls == lat[f"{tag}_gt"]).mean()
+        # exact lattices are full of kNN distance ties; scipy's tie order is implementation-defined
+        assert abs(acc - float(lat[f"{tag}_acc"])) < 0.01, (tag, acc, float(lat[f"{tag}_acc"]))
+        if tag.endswith("j1"):
+            assert (cls == lat[f"{tag}_classes"]).mean() > 0.995
+
+
+def test_orientation_mst(golden):
+    lat = golden("lattice")
+    pos = lat["n9_j1_pos"]
+    nbr = O.knn_graph_noself(pos, 12)
+    n = O.pca_normals_unoriented(pos, nbr)
+    n = O.orient_normals_mst(pos, n, nbr)
+    agree = np.abs((n * lat["n9_j1_n"]).sum(1))
+    signs = np.sign((n * lat["n9_j1_n"]).sum(1))
+    assert np.percentile(agree, 1) > 0.99
+    assert (signs > 0).mean() > 0.99
+
+
+def test_mesh_update(golden):
+    m = golden("mesh_update")
+    v1 = O.mesh_update(m["v"], m["f"], m["n"], k=1)
+    np.testing.assert_allclose(v1, m["v_k1"], rtol=0, atol=1e-12)
+    v15 = O.mesh_update(m["v"], m["f"], m["n"], k=15)
+    np.testing.assert_allclose(v15, m["v_k15"], rtol=0, atol=1e-10)
+
+
+def test_metrics(golden):
+    m = golden("metrics")
+    np.testing.assert_allclose(O.chamfer(m["a"], m["b"]), m["chamfer"], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(O.paper_distance(m["a"], m["b"]), m["paper"], rtol=1e-5, atol=1e-9)
