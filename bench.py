@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--k-update", type=int, default=8)
     ap.add_argument("--cpu-sample", type=int, default=200_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seeding", action="store_true", help="cap each kNN search at last iteration's list")
     ap.add_argument("--profile-steps", type=int, default=5, help="extra per-kernel timed iterations (HIP events)")
     args = ap.parse_args()
 
@@ -110,6 +111,7 @@ def main():
     d = 2 * float(proc.meanEdgeLength())
     fused = proc._fused_for(max(args.k, args.k_update))
     fused.load(proc.graph.pos, proc.graph.n)
+    fused.set_seeding(args.seeding)
     params = nat.make_params(k=args.k, k_update=args.k_update, d=d)
 
     for _ in range(args.warmup):

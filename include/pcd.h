@@ -75,6 +75,11 @@ int pcd_grid_perm(const pcd_grid* g, int32_t* perm, void* stream);
 int pcd_knn(const pcd_grid* g, const float* q, int64_t nq, int k, void* idx_out, int idx_bits, int sorted_ids,
             int exclude_self, float* d2_out, void* stream);
 
+/* Diagnostic: total work of a kNN(k) pass over q (spatial-order ids), summed over queries into out6 (device u64):
+ * cells considered, cells probed in the hash, cells found, candidates scanned, sorted inserts (k < 16) or
+ * buffer flushes (k >= 16), extra rings. */
+int pcd_knn_stats(const pcd_grid* g, const float* q, int64_t nq, int k, unsigned long long* out6, void* stream);
+
 /* ------------------------------------------------------------------ tensor voting (H5-H7, H15) */
 /* CSR selection: segment r has centre ci[r] and neighbours nbr[off[r] .. off[r+1]); all int64 (torch long). */
 int pcd_nvt_csr(const float* pos, const float* n, int64_t npts, const int64_t* ci, const int64_t* off,
@@ -136,6 +141,11 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
  * are those of the LAST iteration's NVT2; f_n is the last smoothed normal field (= n after iterate). */
 int pcd_denoiser_store(pcd_denoiser* dn, float* pos, float* n, int64_t* classes, float* edge_vectors,
                        void* stream);
+/* Seeded search (default off): iterations after the first cap the acceptance threshold at the largest key of
+ * the previous iteration's stored list.  Results are identical either way; it only changes the work done.
+ * reset_seed forgets the stored list, so the next iterate() runs unseeded. */
+int pcd_denoiser_set_seeding(pcd_denoiser* dn, int enable);
+int pcd_denoiser_reset_seed(pcd_denoiser* dn);
 /* Profiling aid: elapsed ms of each kernel class in the last iterate() when timing was enabled. */
 int pcd_denoiser_set_timing(pcd_denoiser* dn, int enable);
 int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n_written);

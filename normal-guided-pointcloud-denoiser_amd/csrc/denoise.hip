@@ -52,23 +52,44 @@ __global__ void k_store(const float4* __restrict__ pos_s, const float4* __restri
 }
 
 // K1: kNN + NVT1 + VU smoothing.
-template <int K>
+// SEED (iterations after the first): the largest key of last
+// iteration's list (kstore distinct snapshot points) caps the acceptance threshold from the first candidate on.
+template <int K, bool SEED>
 __global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __restrict__ pos,
                                                    const float4* __restrict__ nrm, int64_t N, int k, int kstore,
                                                    float rho, float tau, float damp, int32_t* __restrict__ idx,
-                                                   float4* __restrict__ fn) {
+                                                   float4* __restrict__ fn, int* __restrict__ err) {
     const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     if (i >= N) return;
     const float4 p4 = pos[i];
     const Vec3 vi = v3(p4.x, p4.y, p4.z);
     TopK<K> tk;
-    knn_search<K>(g, vi, tk);
+    unsigned long long cap = kInfKey;
+    if constexpr (SEED) {           // max key of last iteration's list >= this iteration's kstore-th key
+        cap = 0ull;
+#pragma unroll
+        for (int t = 0; t < K; ++t) {
+            if (t < kstore) {
+                const uint32_t sd = (uint32_t)idx[(int64_t)t * N + i];
+                const unsigned long long c = cand_key<false>(vi, g.pts[sd], sd);
+                cap = c > cap ? c : cap;
+            }
+        }
+        cap += 1ull;                 // acceptance is `key < cap`: keep the seed list's own largest key
+    }
+    knn_search<K, false>(g, vi, tk, cap);
     int l[K];
+    bool bad = false;
 #pragma unroll
     for (int t = 0; t < K; ++t) {
         l[t] = tk.idx(t);
-        if (t < kstore) idx[(int64_t)t * N + i] = l[t];
+        if (t < kstore) {
+            // a list entry that is not a point would be an internal error: record it, never fault on it
+            if ((uint32_t)l[t] >= (uint32_t)N) { bad = true; l[t] = (int)i; }
+            idx[(int64_t)t * N + i] = l[t];
+        }
     }
+    if (bad) atomicOr(err, 1);
     const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho);
     float w[3], V[3][3];
     eigh3(T, w, V);
@@ -188,6 +209,9 @@ struct pcd_denoiser {
     uint8_t* cls = nullptr;
     RedC* part = nullptr;
     float* gscal = nullptr;       // 4 floats per phase: centre xyz, delta bits
+    int* err = nullptr;           // device error word (invalid kNN entries), checked by store()
+    int seed_cols = 0;            // columns of idx holding a valid kNN list of the snapshot (0: none yet)
+    bool seeding = false;         // use the stored list as an acceptance cap (pcd_denoiser_set_seeding)
     bool loaded = false, iterated = false;
     bool timing = false;
     std::vector<hipEvent_t> ev;
@@ -218,7 +242,8 @@ int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out) {
               hipMalloc(&dn->idx, (int64_t)k_max * N * sizeof(int32_t)) == hipSuccess &&
               hipMalloc(&dn->cls, N) == hipSuccess &&
               hipMalloc(&dn->part, kNumPart * sizeof(RedC)) == hipSuccess &&
-              hipMalloc(&dn->gscal, 16 * sizeof(float)) == hipSuccess;
+              hipMalloc(&dn->gscal, 16 * sizeof(float)) == hipSuccess &&
+              hipMalloc(&dn->err, sizeof(int)) == hipSuccess && hipMemset(dn->err, 0, sizeof(int)) == hipSuccess;
     if (!ok) {
         pcd_denoiser_destroy(dn);
         return fail(PCD_ERR_OOM, "pcd_denoiser_create: device allocation");
@@ -231,6 +256,7 @@ int pcd_denoiser_destroy(pcd_denoiser* dn) {
     if (!dn) return PCD_OK;
     (void)(void)hipFree(dn->pos[0]); (void)hipFree(dn->pos[1]); (void)hipFree(dn->nrm); (void)hipFree(dn->fn); (void)hipFree(dn->edge);
     (void)(void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part); (void)hipFree(dn->gscal);
+    (void)hipFree(dn->err);
     for (auto e : dn->ev) (void)hipEventDestroy(e);
     delete dn;
     return PCD_OK;
@@ -244,6 +270,18 @@ int pcd_denoiser_load(pcd_denoiser* dn, const float* pos, const float* n, void* 
     dn->cur = 0;
     dn->loaded = true;
     dn->iterated = false;
+    return PCD_OK;
+}
+
+int pcd_denoiser_reset_seed(pcd_denoiser* dn) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    dn->seed_cols = 0;
+    return PCD_OK;
+}
+
+int pcd_denoiser_set_seeding(pcd_denoiser* dn, int enable) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    dn->seeding = enable != 0;
     return PCD_OK;
 }
 
@@ -286,26 +324,31 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
     hipStream_t st = as_stream(stream);
     const int64_t N = dn->n;
     const int kstore = std::max(p->k, p->k_update);
-    const int cap = knn_cap(kstore) < 8 ? 8 : knn_cap(kstore);
+    const int cap = kstore <= 8 ? 8 : kstore <= 16 ? 16 : kstore <= 32 ? 32 : 64;
     const dim3 blk(256), grd((unsigned)cdiv(N, 256));
     const GridView gv = dn->g->view;
     for (int it = 0; it < iterations; ++it) {
         const bool rec = dn->timing && it == iterations - 1;
         if (rec) PCD_HIP(hipEventRecord(dn->ev[0], st));
         float4* P = dn->pos[dn->cur];
+        const bool seed = dn->seeding && dn->seed_cols >= kstore;
 #define PCD_K1(C) \
-    case C: hipLaunchKernelGGL(k_knn_nvt1<C>, grd, blk, 0, st, gv, P, dn->nrm, N, p->k, kstore, p->rho, p->tau, p->damp, dn->idx, dn->fn); break;
+    case C:                                                                                                          \
+        if (seed) hipLaunchKernelGGL((k_knn_nvt1<C, true>), grd, blk, 0, st, gv, P, dn->nrm, N, p->k, kstore, p->rho, p->tau, p->damp, dn->idx, dn->fn, dn->err); \
+        else hipLaunchKernelGGL((k_knn_nvt1<C, false>), grd, blk, 0, st, gv, P, dn->nrm, N, p->k, kstore, p->rho, p->tau, p->damp, dn->idx, dn->fn, dn->err); \
+        break;
         switch (cap) {
-            PCD_K1(8) PCD_K1(16) PCD_K1(24) PCD_K1(32) PCD_K1(48) PCD_K1(64)
+            PCD_K1(8) PCD_K1(16) PCD_K1(32) PCD_K1(64)
             default: return fail(PCD_ERR_ARG, "unsupported k");
         }
 #undef PCD_K1
         PCD_LAUNCH_CHECK();
+        dn->seed_cols = kstore;
         if (rec) PCD_HIP(hipEventRecord(dn->ev[1], st));
 #define PCD_K2(C) \
     case C: hipLaunchKernelGGL(k_nvt2<C>, grd, blk, 0, st, P, dn->fn, dn->idx, N, p->k, p->rho, p->class_scale, dn->cls, dn->edge); break;
         switch (cap) {
-            PCD_K2(8) PCD_K2(16) PCD_K2(24) PCD_K2(32) PCD_K2(48) PCD_K2(64)
+            PCD_K2(8) PCD_K2(16) PCD_K2(32) PCD_K2(64)
             default: return fail(PCD_ERR_ARG, "unsupported k");
         }
 #undef PCD_K2
@@ -354,6 +397,10 @@ int pcd_denoiser_store(pcd_denoiser* dn, float* pos, float* n, int64_t* classes,
     hipLaunchKernelGGL(k_store, dim3((unsigned)cdiv(dn->n, 256)), dim3(256), 0, as_stream(stream), dn->pos[dn->cur],
                        dn->nrm, dn->cls, dn->edge, dn->g->perm, dn->n, pos, n, classes, edge_vectors);
     PCD_LAUNCH_CHECK();
+    int err = 0;
+    PCD_HIP(hipMemcpyAsync(&err, dn->err, sizeof(int), hipMemcpyDeviceToHost, as_stream(stream)));
+    PCD_HIP(hipStreamSynchronize(as_stream(stream)));
+    if (err) return fail(PCD_ERR_STATE, "pcd_denoiser: the kNN kernel produced an invalid neighbour index");
     return PCD_OK;
 }
 

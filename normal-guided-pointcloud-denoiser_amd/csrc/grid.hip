@@ -76,7 +76,7 @@ __global__ void k_gather_sorted(const float* __restrict__ xyz, const int32_t* __
     const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (r >= n) return;
     const int64_t i = perm[r];
-    pts[r] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], 0.f);
+    pts[r] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], __uint_as_float((uint32_t)i));
 }
 
 __global__ void k_count_starts(const unsigned long long* __restrict__ keys, int64_t n, unsigned long long* count) {
@@ -105,25 +105,24 @@ __global__ void k_insert(const unsigned long long* __restrict__ keys, int64_t n,
 }
 
 // ------------------------------------------------------------------ query kernels
-template <int K, bool IDX64>
+template <int K, bool ORIG>
 __global__ __launch_bounds__(256) void k_knn(GridView g, const float* __restrict__ q, int64_t nq, int kq, int k,
-                                              void* __restrict__ idx_out, const int32_t* __restrict__ perm,
-                                              int exclude_self, float* __restrict__ d2_out) {
+                                              void* __restrict__ idx_out, int idx64, int exclude_self,
+                                              float* __restrict__ d2_out) {
     const int64_t nb = gridDim.x;
     const int64_t b = xcd_block(blockIdx.x, nb);
     const int64_t i = b * blockDim.x + threadIdx.x;
     if (i >= nq) return;
     const Vec3 qi = v3(q[3 * i], q[3 * i + 1], q[3 * i + 2]);
     TopK<K> tk;
-    knn_search<K>(g, qi, tk);
+    knn_search<K, ORIG>(g, qi, tk);
     int w = 0;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        int id = tk.idx(j);
-        if (perm) id = (j < kq) ? perm[id] : -1;
+        const int id = tk.idx(j);
         const bool take = (w < k) && (j < kq) && !(exclude_self && id == i);
         if (take) {
-            if (IDX64) reinterpret_cast<int64_t*>(idx_out)[i * k + w] = id;
+            if (idx64) reinterpret_cast<int64_t*>(idx_out)[i * k + w] = id;
             else reinterpret_cast<int32_t*>(idx_out)[i * k + w] = id;
             if (d2_out) d2_out[i * k + w] = tk.d2(j);
             ++w;
@@ -131,34 +130,33 @@ __global__ __launch_bounds__(256) void k_knn(GridView g, const float* __restrict
     }
 }
 
-__global__ void k_nn1(GridView g, const float* __restrict__ q, int64_t nq, const int32_t* __restrict__ perm,
-                      float* __restrict__ d2_out, int64_t* __restrict__ idx_out) {
+__global__ void k_nn1(GridView g, const float* __restrict__ q, int64_t nq, float* __restrict__ d2_out, int64_t* __restrict__ idx_out) {
     const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     if (i >= nq) return;
     TopK<1> tk;
-    knn_search<1>(g, v3(q[3 * i], q[3 * i + 1], q[3 * i + 2]), tk);
+    knn_search<1, true>(g, v3(q[3 * i], q[3 * i + 1], q[3 * i + 2]), tk);
     if (d2_out) d2_out[i] = tk.d2(0);
-    if (idx_out) idx_out[i] = perm[tk.idx(0)];
+    if (idx_out) idx_out[i] = tk.idx(0);
 }
 
 // K capacity ladder of the register top-k lists.
-static const int kCaps[] = {1, 4, 8, 13, 16, 24, 32, 48, 64};
+static const int kCaps[] = {1, 4, 8, 13, 16, 32, 64};
 int knn_cap(int k) {
     for (int c : kCaps)
         if (k <= c) return c;
     return -1;
 }
 
-template <bool IDX64>
-static int launch_knn(const GridView& g, const float* q, int64_t nq, int kq, int k, void* idx, const int32_t* perm,
+template <bool ORIG>
+static int launch_knn(const GridView& g, const float* q, int64_t nq, int kq, int k, void* idx, int idx64,
                       int excl, float* d2, hipStream_t st) {
     const int cap = knn_cap(kq);
     const dim3 blk(256), grd((unsigned)cdiv(nq, 256));
 #define PCD_KNN_CASE(C) \
-    case C: hipLaunchKernelGGL((k_knn<C, IDX64>), grd, blk, 0, st, g, q, nq, kq, k, idx, perm, excl, d2); break;
+    case C: hipLaunchKernelGGL((k_knn<C, ORIG>), grd, blk, 0, st, g, q, nq, kq, k, idx, idx64, excl, d2); break;
     switch (cap) {
-        PCD_KNN_CASE(1) PCD_KNN_CASE(4) PCD_KNN_CASE(8) PCD_KNN_CASE(13) PCD_KNN_CASE(16) PCD_KNN_CASE(24)
-        PCD_KNN_CASE(32) PCD_KNN_CASE(48) PCD_KNN_CASE(64)
+        PCD_KNN_CASE(1) PCD_KNN_CASE(4) PCD_KNN_CASE(8) PCD_KNN_CASE(13) PCD_KNN_CASE(16) PCD_KNN_CASE(32)
+        PCD_KNN_CASE(64)
         default: return fail(PCD_ERR_ARG, "pcd_knn: k larger than pcd_max_k()");
     }
 #undef PCD_KNN_CASE
@@ -336,10 +334,9 @@ int pcd_knn(const pcd_grid* g, const float* q, int64_t nq, int k, void* idx_out,
     if (nq == 0) return PCD_OK;
     PCD_CHECK_ARG(q && idx_out, "null query / output");
     PCD_CHECK_ARG(!(exclude_self && sorted_ids), "exclude_self requires original ids");
-    const int32_t* perm = sorted_ids ? nullptr : g->perm;
     hipStream_t st = as_stream(stream);
-    return idx_bits == 64 ? launch_knn<true>(g->view, q, nq, kq, k, idx_out, perm, exclude_self, d2_out, st)
-                          : launch_knn<false>(g->view, q, nq, kq, k, idx_out, perm, exclude_self, d2_out, st);
+    return sorted_ids ? launch_knn<false>(g->view, q, nq, kq, k, idx_out, idx_bits == 64, exclude_self, d2_out, st)
+                      : launch_knn<true>(g->view, q, nq, kq, k, idx_out, idx_bits == 64, exclude_self, d2_out, st);
 }
 
 int pcd_nn_dist(const pcd_grid* g, const float* q, int64_t nq, float* d2_out, int64_t* idx_out, void* stream) {
@@ -347,7 +344,7 @@ int pcd_nn_dist(const pcd_grid* g, const float* q, int64_t nq, float* d2_out, in
     if (nq == 0) return PCD_OK;
     PCD_CHECK_ARG(q != nullptr, "null query");
     hipLaunchKernelGGL(k_nn1, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, as_stream(stream), g->view, q, nq,
-                       g->perm, d2_out, idx_out);
+                       d2_out, idx_out);
     PCD_LAUNCH_CHECK();
     return PCD_OK;
 }

@@ -50,14 +50,32 @@ PCD_DEV int cell_coord(float p, float o, float inv_h) {
 
 static constexpr unsigned long long kInfKey = (0x7F800000ull << 32) | 0xFFFFFFFFull;
 
+// Sorted register list of the K best candidate keys.  `cap` is an optional acceptance bound known to be >= the
+// true k-th key (a seed: the k-th distance to any k distinct snapshot points); it prunes cells and rejects
+// candidates before the list has filled.
+#ifdef PCD_KNN_STATS  // diagnostic build only (stats.hip): per-query work counters
+#define PCD_KSTAT(tk, i, v) ((tk).stat[i] += (v))
+#else
+#define PCD_KSTAT(tk, i, v) ((void)0)
+#endif
+
 template <int K>
 struct TopK {
     unsigned long long key[K];
-    PCD_DEV void init() {
+    unsigned long long cap;
+#ifdef PCD_KNN_STATS
+    unsigned stat[6];  // cells considered, cells probed, cells found, candidates, inserts, rings
+#endif
+    PCD_DEV void init(unsigned long long c = kInfKey) {
 #pragma unroll
         for (int i = 0; i < K; ++i) key[i] = kInfKey;
+        cap = c;
+#ifdef PCD_KNN_STATS
+        for (int i = 0; i < 6; ++i) stat[i] = 0;
+#endif
     }
-    PCD_DEV float kth() const { return __uint_as_float((unsigned)(key[K - 1] >> 32)); }
+    PCD_DEV unsigned long long limit() const { return key[K - 1] < cap ? key[K - 1] : cap; }
+    PCD_DEV float kth() const { return __uint_as_float((unsigned)(limit() >> 32)); }
     PCD_DEV void insert(unsigned long long c) {
 #pragma unroll
         for (int j = K - 1; j > 0; --j) {
@@ -76,34 +94,44 @@ PCD_DEV float dist2(Vec3 q, float4 p) {
     return __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
 }
 
-template <int K>
+// Candidate key: d² bits in the high word; the low word is the snapshot point's ORIGINAL index (ORIG, kept in
+// pts[r].w at build; ties then break by caller index) or its rank r in the Morton-sorted snapshot (!ORIG: the
+// fused loop works in sorted order, where rank == working index).
+template <bool ORIG>
+PCD_DEV unsigned long long cand_key(Vec3 q, float4 p, uint32_t r) {
+    return ((unsigned long long)__float_as_uint(dist2(q, p)) << 32) | (ORIG ? __float_as_uint(p.w) : r);
+}
+
+template <int K, bool ORIG>
 PCD_DEV void scan_range(const float4* __restrict__ pts, uint32_t s, uint32_t e, Vec3 q, TopK<K>& tk) {
     uint32_t r = s;
     for (; r + 1 < e; r += 2) {  // two loads in flight per lane
         const float4 p0 = pts[r], p1 = pts[r + 1];
-        const unsigned long long c0 = ((unsigned long long)__float_as_uint(dist2(q, p0)) << 32) | r;
-        const unsigned long long c1 = ((unsigned long long)__float_as_uint(dist2(q, p1)) << 32) | (r + 1);
-        if (c0 < tk.key[K - 1]) tk.insert(c0);
-        if (c1 < tk.key[K - 1]) tk.insert(c1);
+        const unsigned long long c0 = cand_key<ORIG>(q, p0, r);
+        const unsigned long long c1 = cand_key<ORIG>(q, p1, r + 1);
+        if (c0 < tk.limit()) { tk.insert(c0); PCD_KSTAT(tk, 4, 1); }
+        if (c1 < tk.limit()) { tk.insert(c1); PCD_KSTAT(tk, 4, 1); }
     }
     if (r < e) {
-        const float4 p0 = pts[r];
-        const unsigned long long c0 = ((unsigned long long)__float_as_uint(dist2(q, p0)) << 32) | r;
-        if (c0 < tk.key[K - 1]) tk.insert(c0);
+        const unsigned long long c0 = cand_key<ORIG>(q, pts[r], r);
+        if (c0 < tk.limit()) { tk.insert(c0); PCD_KSTAT(tk, 4, 1); }
     }
+    PCD_KSTAT(tk, 3, e - s);
 }
 
 PCD_DEV float axis_gap(float q, float lo, float hi) { return fmaxf(fmaxf(lo - q, q - hi), 0.f); }
 
 // Scan one cell unless its box is provably farther than the current k-th candidate.
-template <int K>
+template <int K, bool ORIG>
 PCD_DEV void visit_cell(const GridView& g, Vec3 q, int cx, int cy, int cz, TopK<K>& tk) {
     const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
     const float gx = axis_gap(q.x, lx, lx + g.h), gy = axis_gap(q.y, ly, ly + g.h), gz = axis_gap(q.z, lz, lz + g.h);
     const float box = gx * gx + gy * gy + gz * gz;
+    PCD_KSTAT(tk, 0, 1);
     if (box > tk.kth() * 1.00001f + 1e-30f) return;
     uint32_t s, e;
-    if (cell_range(g, cx, cy, cz, s, e)) scan_range<K>(g.pts, s, e, q, tk);
+    PCD_KSTAT(tk, 1, 1);
+    if (cell_range(g, cx, cy, cz, s, e)) { PCD_KSTAT(tk, 2, 1); scan_range<K, ORIG>(g.pts, s, e, q, tk); }
 }
 
 // 3x3x3 neighbourhood: centre, 6 faces, 12 edges, 8 corners (closest cells first -> the k-th distance
@@ -137,23 +165,24 @@ PCD_DEV bool search_done(const GridView& g, Vec3 q, int cx, int cy, int cz, int 
     return exhausted || kth <= bound * bound * 0.99998f;
 }
 
-// Exact top-K of the snapshot for query q.
-template <int K>
-PCD_DEV void knn_search(const GridView& g, Vec3 q, TopK<K>& tk) {
-    tk.init();
+// Exact top-K of the snapshot for query q (entries beyond the seed's rank are only valid when cap == inf).
+template <int K, bool ORIG>
+PCD_DEV void knn_search(const GridView& g, Vec3 q, TopK<K>& tk, unsigned long long cap = kInfKey) {
+    tk.init(cap);
     int cx = min(max(cell_coord(q.x, g.ox, g.inv_h), 0), g.dx - 1);
     int cy = min(max(cell_coord(q.y, g.oy, g.inv_h), 0), g.dy - 1);
     int cz = min(max(cell_coord(q.z, g.oz, g.inv_h), 0), g.dz - 1);
 #pragma unroll 1
     for (int t = 0; t < 27; ++t)
-        visit_cell<K>(g, q, cx + kRing1[t][0], cy + kRing1[t][1], cz + kRing1[t][2], tk);
+        visit_cell<K, ORIG>(g, q, cx + kRing1[t][0], cy + kRing1[t][1], cz + kRing1[t][2], tk);
     int R = 1;
 #pragma unroll 1
     while (!search_done(g, q, cx, cy, cz, R, tk.kth())) {
         ++R;
+        PCD_KSTAT(tk, 5, 1);
         if (R > 24) {  // pathological outlier: exhaustive scan (correct, slow, never hit on denoise inputs)
-            tk.init();
-            scan_range<K>(g.pts, 0, (uint32_t)g.n, q, tk);
+            tk.init(cap);
+            scan_range<K, ORIG>(g.pts, 0, (uint32_t)g.n, q, tk);
             return;
         }
 #pragma unroll 1
@@ -163,7 +192,7 @@ PCD_DEV void knn_search(const GridView& g, Vec3 q, TopK<K>& tk) {
                 const bool rim = (dz == -R || dz == R || dy == -R || dy == R);
                 const int step = rim ? 1 : 2 * R;
 #pragma unroll 1
-                for (int dx = -R; dx <= R; dx += step) visit_cell<K>(g, q, cx + dx, cy + dy, cz + dz, tk);
+                for (int dx = -R; dx <= R; dx += step) visit_cell<K, ORIG>(g, q, cx + dx, cy + dy, cz + dz, tk);
             }
         }
     }

@@ -46,6 +46,7 @@ _SIGS = {
     "pcd_grid_get_info": (c_int, [c_void_p, POINTER(_GridInfo)]),
     "pcd_grid_perm": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_knn": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "pcd_knn_stats": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     "pcd_nvt_csr": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p,
                             c_void_p, c_void_p]),
     "pcd_vu_smooth": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p, c_void_p]),
@@ -62,6 +63,8 @@ _SIGS = {
     "pcd_denoiser_iterate": (c_int, [c_void_p, POINTER(DenoiseParams), c_int, c_void_p]),
     "pcd_denoiser_store": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pcd_denoiser_set_timing": (c_int, [c_void_p, c_int]),
+    "pcd_denoiser_reset_seed": (c_int, [c_void_p]),
+    "pcd_denoiser_set_seeding": (c_int, [c_void_p, c_int]),
     "pcd_denoiser_get_timing": (c_int, [c_void_p, POINTER(c_float), c_int, POINTER(c_int)]),
     "pcd_orient_normals_mst": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64]),
     "pcd_host_eigh3": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
@@ -168,14 +171,25 @@ class Grid:
         check(lib().pcd_grid_perm(self.handle, ptr(out), c_void_p(stream_ptr())), "pcd_grid_perm")
         return out
 
-    def knn(self, q: torch.Tensor, k: int, exclude_self: bool = False, with_d2: bool = False, idx_bits: int = 64):
+    def knn(self, q: torch.Tensor, k: int, exclude_self: bool = False, with_d2: bool = False, idx_bits: int = 64,
+            sorted_ids: bool = False):
         q = f32(q)
         nq = q.size(0)
         idx = torch.empty((nq, k), dtype=torch.int64 if idx_bits == 64 else torch.int32, device=q.device)
         d2 = torch.empty((nq, k), dtype=torch.float32, device=q.device) if with_d2 else None
-        check(lib().pcd_knn(self.handle, ptr(q), nq, int(k), ptr(idx), idx_bits, 0, int(exclude_self), ptr(d2),
-                            c_void_p(stream_ptr())), "pcd_knn")
+        check(lib().pcd_knn(self.handle, ptr(q), nq, int(k), ptr(idx), idx_bits, int(sorted_ids), int(exclude_self),
+                            ptr(d2), c_void_p(stream_ptr())), "pcd_knn")
         return (idx, d2) if with_d2 else idx
+
+    def knn_stats(self, q: torch.Tensor, k: int) -> dict:
+        """Per-query averages of the kNN search work (diagnostic build of the search)."""
+        q = f32(q)
+        out = torch.zeros(6, dtype=torch.int64, device=q.device)
+        check(lib().pcd_knn_stats(self.handle, ptr(q), q.size(0), int(k), ptr(out), c_void_p(stream_ptr())),
+              "pcd_knn_stats")
+        v = out.cpu().double() / max(q.size(0), 1)
+        names = ["cells_considered", "cells_probed", "cells_found", "candidates", "inserts", "extra_rings"]
+        return {nm: round(float(x), 2) for nm, x in zip(names, v)}
 
     def nn(self, q: torch.Tensor):
         q = f32(q)
@@ -213,6 +227,12 @@ class FusedDenoiser:
     def store(self, pos=None, n=None, classes=None, edge_vectors=None):
         check(lib().pcd_denoiser_store(self.handle, ptr(pos), ptr(n), ptr(classes), ptr(edge_vectors),
                                        c_void_p(stream_ptr())), "pcd_denoiser_store")
+
+    def set_seeding(self, enable=True):
+        check(lib().pcd_denoiser_set_seeding(self.handle, int(bool(enable))), "pcd_denoiser_set_seeding")
+
+    def reset_seed(self):
+        check(lib().pcd_denoiser_reset_seed(self.handle), "pcd_denoiser_reset_seed")
 
     def set_timing(self, on: bool):
         check(lib().pcd_denoiser_set_timing(self.handle, int(on)), "pcd_denoiser_set_timing")
