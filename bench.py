@@ -41,6 +41,11 @@ from Pointcloud.Modules.Processor import Processor  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
+def knn_cap(k):
+    """Register list size the fused kernel is instantiated with (pcd_denoiser_iterate)."""
+    return 8 if k <= 8 else 16 if k <= 16 else 32 if k <= 32 else 64
+
+
 def b_alg_iteration(k, ku):
     """Algorithmic bytes / point / iteration: 148 + 72k + 60k_u."""
     return 148 + 72 * k + 60 * ku
@@ -66,7 +71,10 @@ def make_cloud(n, seed, dev, sigma_frac=0.005):
 def cpu_baseline(k, ku, sample_points, seed=99):
     """The oracle (numpy/scipy restatement of the reference, cKDTree workers=1) on a bounded sample."""
     from oracle import pcd_oracle as O
-    threads = os.cpu_count() or 1
+    # the host share this process may use: affinity mask, capped by OMP_NUM_THREADS (16 on the GPU box)
+    threads = len(os.sched_getaffinity(0))
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
     torch.set_num_threads(threads)
     pos, nrm, _ = make_cloud(sample_points, seed, torch.device("cpu"))
     pos, nrm = pos.numpy(), nrm.numpy()
@@ -89,7 +97,7 @@ def main():
     ap.add_argument("--points", type=int, default=10_000_000)
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--k-update", type=int, default=8)
-    ap.add_argument("--cpu-sample", type=int, default=200_000)
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seeding", action="store_true", help="cap each kNN search at last iteration's list")
     ap.add_argument("--profile-steps", type=int, default=5, help="extra per-kernel timed iterations (HIP events)")
@@ -156,7 +164,9 @@ def main():
         try:
             tj = json.load(open(tfile))
             if tj.get("points") == args.points and tj.get("k") == args.k:
-                traffic = tj.get("knn_nvt1_hbm_bytes_per_launch")
+                for e in tj["kernels"].get(f"k_knn_nvt1<{knn_cap(max(args.k, args.k_update))}, "
+                                           f"{'true' if args.seeding else 'false'}>", []):
+                    traffic = e.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     iter_alg = b_alg_iteration(args.k, args.k_update) * args.points

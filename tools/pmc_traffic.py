@@ -1,0 +1,62 @@
+"""Turn two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; csv output) into profiles/traffic.json.
+
+HBM bytes per launch of each kernel = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: the counters are in KiB, and on gfx950
+FETCH_SIZE tallies half the bytes of 16-B-per-lane reads (MI355X_MICROARCH.md, HBM / rocprofv3 section).  The raw
+values are kept next to the corrected ones.
+
+usage: python tools/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> <points> <k> [out.json]
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def per_kernel(path, counter):
+    vals = defaultdict(list)
+    with open(path, newline="") as fh:
+        for row in csv.DictReader(fh):
+            if row.get("Counter_Name") != counter:
+                continue
+            name = row["Kernel_Name"]
+            vals[name].append(float(row["Counter_Value"]))
+    return vals
+
+
+def short(name):
+    base = name.split("(")[0]
+    return base.replace("void ", "").replace("pcd::", "").strip()
+
+
+def main():
+    fetch_csv, write_csv = sys.argv[1], sys.argv[2]
+    points, k = int(sys.argv[3]), int(sys.argv[4])
+    out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(__file__), "..", "profiles", "traffic.json")
+    fetch = per_kernel(fetch_csv, "FETCH_SIZE")
+    write = per_kernel(write_csv, "WRITE_SIZE")
+    kernels = {}
+    for name in sorted(set(fetch) | set(write)):
+        if "pcd::" not in name:
+            continue
+        f = fetch.get(name, [])
+        w = write.get(name, [])
+        fk = sum(f) / len(f) if f else None
+        wk = sum(w) / len(w) if w else None
+        entry = {"launches_fetch": len(f), "launches_write": len(w),
+                 "fetch_size_kib_raw": fk, "write_size_kib_raw": wk}
+        if fk is not None and wk is not None:
+            entry["hbm_bytes_per_launch"] = (2.0 * fk + wk) * 1024.0
+        kernels.setdefault(short(name), []).append(dict(entry, symbol=name))
+    res = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, csv; "
+                     "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch (gfx950 FETCH_SIZE counts half)",
+           "points": points, "k": k, "kernels": kernels}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    for kname, v in kernels.items():
+        for e in v:
+            print(kname, e.get("hbm_bytes_per_launch"), e["launches_fetch"], e["launches_write"])
+
+
+if __name__ == "__main__":
+    main()
