@@ -10,9 +10,11 @@ One "step" = one full iteration of Processor.denoise's loop body on device-resid
 frozen snapshot -> NVT1 + VU smoothing -> NVT2 + classes -> flat (global reduce) / edge / corner updates.
 Excluded (one-time): snapshot/grid build, initial normals, mean edge length l, data synthesis.
 
-Multi-GPU: every rank denoises its own P-point cloud (seed + rank) -- weak scaling, no data-path collective; the
-timed region is bracketed by barrier + synchronize and the max over ranks is reported.  The spatial-slab mode
-with RCCL halo exchange is exercised by tests/test_dist.py.
+Multi-GPU (BASELINE configs[4]): one global cloud of N x P points is cut into N spatial slabs
+along its longest axis; each rank denoises its slab and exchanges halo state with its slab neighbours over RCCL
+(pcd_slab), plus two scalar all-reduces per flat phase -- weak scaling (P points per GPU).  --replicas instead
+runs N independent P-point clouds.  The timed region is bracketed by barrier + synchronize and the max over
+ranks is reported.
 
 The JSON line carries `roofline` for the dominant kernel (fused kNN + NVT1, HIP events on its own stream) and
 `cpu_baseline` (the oracle restatement on host cores over a bounded sample; rank 0, N = 1 only).
@@ -101,36 +103,57 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seeding", action="store_true", help="cap each kNN search at last iteration's list")
     ap.add_argument("--profile-steps", type=int, default=5, help="extra per-kernel timed iterations (HIP events)")
+    ap.add_argument("--replicas", action="store_true",
+                    help="N > 1: independent clouds per rank instead of spatial slabs of one global cloud")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL ("nccl") between GPUs; PCD_BENCH_BACKEND=gloo only to rehearse several ranks on one GPU
+        backend = os.environ.get("PCD_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    mode = "single" if world == 1 else ("replicas" if args.replicas else "slab")
 
-    pos, nrm, diag = make_cloud(args.points, 2 + rank, dev)
-    pc = Pointcloud(pos, nrm)
-    proc = Processor(pc, k_hint=args.k)
-    d = 2 * float(proc.meanEdgeLength())
-    fused = proc._fused_for(max(args.k, args.k_update))
-    fused.load(proc.graph.pos, proc.graph.n)
-    fused.set_seeding(args.seeding)
-    params = nat.make_params(k=args.k, k_update=args.k_update, d=d)
+    if mode == "slab":
+        # one global cloud of world x P points (identical on every rank), cut into spatial slabs with a halo
+        from pcd_slab import SlabDenoiser, TorchTransport
+        pos, nrm, diag = make_cloud(args.points * world, 3, dev)
+        d = 2 * float(Processor(Pointcloud(pos), k_hint=args.k).meanEdgeLength())
+        sd = SlabDenoiser(pos, nrm, max(args.k, args.k_update), transport=TorchTransport(), k_hint=args.k,
+                          seeding=args.seeding)
+        del pos, nrm
+        params = nat.make_params(k=args.k, k_update=args.k_update, d=d)
+        step = lambda: sd.iterate(params, 1)  # noqa: E731
+    else:
+        pos, nrm, diag = make_cloud(args.points, 2 + rank, dev)
+        pc = Pointcloud(pos, nrm)
+        proc = Processor(pc, k_hint=args.k)
+        d = 2 * float(proc.meanEdgeLength())
+        fused = proc._fused_for(max(args.k, args.k_update))
+        fused.load(proc.graph.pos, proc.graph.n)
+        fused.set_seeding(args.seeding)
+        params = nat.make_params(k=args.k, k_update=args.k_update, d=d)
+        step = lambda: fused.iterate(params, 1)  # noqa: E731
 
     for _ in range(args.warmup):
-        fused.iterate(params, 1)
+        step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        fused.iterate(params, 1)
+        step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -145,22 +168,32 @@ def main():
     value = total_points / (ms_per_step / 1e3) / 1e6
 
     # per-kernel timing (HIP events on the launch stream), outside the timed region
-    fused.set_timing(True)
-    slots = []
-    for _ in range(args.profile_steps):
-        fused.iterate(params, 1)
-        slots.append(fused.timing())
-    fused.set_timing(False)
-    slots = np.asarray(slots)
-    knn_ms = float(np.mean(slots[:, 0])) if len(slots) else float("nan")
-    names = ["knn_nvt1", "nvt2", "flat_phase", "edge_phase", "corner_phase", "swap", "end"]
-    kernel_ms = {names[i]: round(float(np.mean(slots[:, i])), 4) for i in range(min(slots.shape[1], 5))} if len(slots) else {}
+    kernel_ms, knn_ms = {}, float("nan")
+    if mode == "slab":
+        sd.check()      # exactness: no k-ball left its rank's slab + halo
+        ks = [sd.iterate_timed(params) for _ in range(args.profile_steps)]
+        if ks:
+            kernel_ms = {key: round(float(np.mean([x[key] for x in ks])), 4) for key in ks[0]}
+            knn_ms = kernel_ms["knn_nvt1"]
+    else:
+        fused.set_timing(True)
+        slots = []
+        for _ in range(args.profile_steps):
+            fused.iterate(params, 1)
+            slots.append(fused.timing())
+        fused.set_timing(False)
+        slots = np.asarray(slots)
+        if len(slots):
+            knn_ms = float(np.mean(slots[:, 0]))
+            names = ["knn_nvt1", "nvt2", "flat_phase", "edge_phase", "corner_phase"]
+            kernel_ms = {names[i]: round(float(np.mean(slots[:, i])), 4) for i in range(min(slots.shape[1], 5))}
 
-    k1_bytes = b_alg_knn_nvt1(args.k) * args.points
+    k1_points = sd.owned_global.numel() if mode == "slab" else args.points
+    k1_bytes = b_alg_knn_nvt1(args.k) * k1_points
     achieved = k1_bytes / (knn_ms / 1e3) / 1e9 if knn_ms == knn_ms else None
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tfile):
+    if os.path.exists(tfile) and mode != "slab":
         try:
             tj = json.load(open(tfile))
             if tj.get("points") == args.points and tj.get("k") == args.k:
@@ -182,11 +215,16 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: bunny-sampled surface + Gaussian noise (sigma=0.005*bbox), analytic normals, seed 2+rank",
-        "config": {"workload": "configs[3] headline substitute: 10M-pt bunny-sampled cloud (xyzrgb_dragon.obj is a "
-                               "missing blob), k=32, k_u=8, 1 iteration per step",
+        "data": "synthetic: bunny-sampled surface + Gaussian noise (sigma=0.005*bbox), analytic normals, "
+                + ("one global cloud (seed 3) cut into spatial slabs" if mode == "slab" else "seed 2+rank"),
+        "config": {"workload": ("configs[4]: synthetic %dM-point bunny-sampled surface, spatial slabs with RCCL halo"
+                                % (total_points // 1_000_000) if mode == "slab" else
+                                "configs[3] headline substitute: 10M-pt bunny-sampled cloud (xyzrgb_dragon.obj is "
+                                "a missing blob)") + ", k=32, k_u=8, 1 iteration per step",
                    "points_per_gpu": args.points, "k": args.k, "k_update": args.k_update,
-                   "global_points": total_points, "parallelism": f"replicas x{world}" if world > 1 else "single"},
+                   "global_points": total_points,
+                   "parallelism": {"single": "single", "replicas": f"replicas x{world}",
+                                   "slab": f"spatial slabs x{world}"}[mode]},
         "iterations_per_sec": round(1e3 / ms_per_step, 2),
         "kernel_ms": kernel_ms,
         "iteration_roofline": {"bound": "hbm", "alg_bytes_per_point": b_alg_iteration(args.k, args.k_update),

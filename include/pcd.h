@@ -59,8 +59,15 @@ typedef struct {
 } pcd_grid_info_t;
 
 /* Build the kNN index over a private copy of xyz[n][3] (fp32 device rows).  cell <= 0 picks the cell edge
- * so an occupied cell holds ~k_hint/2 points.  Synchronises `stream` (one-time construction). */
-int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, void* stream, pcd_grid** out);
+ * so an occupied cell holds ~k_hint/2 points.  origin3 (host, nullable; needs cell > 0) pins the cell lattice:
+ * grids of subsets built on one lattice order their points as subsequences of the full set's order (used by
+ * the spatial slabs, so every rank breaks distance ties like one GPU would).  Synchronises `stream`.
+ * Replaces the KDTree construction of Selector.__init__ (Pointcloud/Modules/Selector.py:138-141). */
+int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, const float* origin3, void* stream,
+                   pcd_grid** out);
+/* The cell lattice pcd_grid_build would pick for xyz (origin = bbox minimum, cell edge), without building. */
+int pcd_grid_params(const float* xyz, int64_t n, int k_hint, float cell, float* origin3, float* cell_out,
+                    void* stream);
 int pcd_grid_destroy(pcd_grid* g);
 int pcd_grid_get_info(const pcd_grid* g, pcd_grid_info_t* out);
 /* perm[r] = original index of the r-th point in the grid's spatial (Morton) order; int32 device [n]. */
@@ -76,9 +83,10 @@ int pcd_knn(const pcd_grid* g, const float* q, int64_t nq, int k, void* idx_out,
             int exclude_self, float* d2_out, void* stream);
 
 /* Diagnostic: total work of a kNN(k) pass over q (spatial-order ids), summed over queries into out6 (device u64):
- * cells considered, cells probed in the hash, cells found, candidates scanned, sorted inserts (k < 16) or
- * buffer flushes (k >= 16), extra rings. */
-int pcd_knn_stats(const pcd_grid* g, const float* q, int64_t nq, int k, unsigned long long* out6, void* stream);
+ * cells considered, cells probed in the hash, cells found, candidates scanned, sorted inserts (variant 0:
+ * per-candidate insertion) or batch merges (variant 1: batched search, k > 8), extra rings. */
+int pcd_knn_stats(const pcd_grid* g, const float* q, int64_t nq, int k, int variant, unsigned long long* out6,
+                  void* stream);
 
 /* ------------------------------------------------------------------ tensor voting (H5-H7, H15) */
 /* CSR selection: segment r has centre ci[r] and neighbours nbr[off[r] .. off[r+1]); all int64 (torch long). */
@@ -149,6 +157,32 @@ int pcd_denoiser_reset_seed(pcd_denoiser* dn);
 /* Profiling aid: elapsed ms of each kernel class in the last iterate() when timing was enabled. */
 int pcd_denoiser_set_timing(pcd_denoiser* dn, int enable);
 int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n_written);
+/* Device error word -> status: PCD_ERR_STATE if a kNN list held an invalid entry or (spatial slabs) a query's
+ * k-ball left the coverage box.  Synchronises `stream`.  store() calls it. */
+int pcd_denoiser_check(pcd_denoiser* dn, void* stream);
+
+/* ---- spatial slabs (multi-GPU): the same loop over a rank's own points with a halo ----
+ * The grid holds the rank's points plus halo snapshot points owned by other ranks.  Only the ACTIVE rows are
+ * queried and updated; the caller keeps the halo rows' state current with pack/unpack + its own transport
+ * (RCCL) between stages, and all-reduces the flat-phase sums (sum) and delta (max) between the PHASE_* stages:
+ *   per iteration: KNN_NVT1 -> exchange FN -> NVT2 -> per phase [flat/new: PHASE_SUM(red=double[4]) ->
+ *   all-reduce sum -> PHASE_CENTRE(red) -> PHASE_MAXDIST(red=float[1]) -> all-reduce max] -> PHASE_APPLY(red or
+ *   null) -> exchange POS -> FINISH.  pcd_denoiser_iterate runs the same sequence with no exchange. */
+enum { PCD_FIELD_POS = 0, PCD_FIELD_NRM = 1, PCD_FIELD_FN = 2 };
+enum { PCD_STAGE_KNN_NVT1 = 0, PCD_STAGE_NVT2 = 1, PCD_STAGE_PHASE_SUM = 2, PCD_STAGE_PHASE_CENTRE = 3,
+       PCD_STAGE_PHASE_MAXDIST = 4, PCD_STAGE_PHASE_APPLY = 5, PCD_STAGE_FINISH = 6 };
+/* rows: device int32 [n_rows] of spatial-order rows (ascending), kept by the caller; null = all rows. */
+int pcd_denoiser_set_rows(pcd_denoiser* dn, const int32_t* rows, int64_t n_rows);
+/* host lo3/hi3: the box the local snapshot covers (null: no check). */
+int pcd_denoiser_set_coverage(pcd_denoiser* dn, const float* lo3, const float* hi3);
+/* one stage; red: device scalars as above (SUM/CENTRE: double[4] Σx,Σy,Σz,count; MAXDIST out / APPLY in:
+ * float[1] delta, nullable = local value). */
+int pcd_denoiser_stage(pcd_denoiser* dn, const pcd_denoise_params* p, int stage, int phase, void* red,
+                       void* stream);
+/* state rows <-> packed device float4 buffers (field PCD_FIELD_*; POS = current positions). */
+int pcd_denoiser_pack(pcd_denoiser* dn, int field, const int32_t* rows, int64_t n, float* out4, void* stream);
+int pcd_denoiser_unpack(pcd_denoiser* dn, int field, const int32_t* rows, int64_t n, const float* in4,
+                        void* stream);
 
 /* ------------------------------------------------------------------ normal orientation (host) */
 /* GraphBuilder.flipNormals: Kruskal MST on cost 1-|n_i·n_j| over the directed edge list (a[e] -> b[e],

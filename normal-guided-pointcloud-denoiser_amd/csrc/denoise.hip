@@ -11,6 +11,12 @@
 //     K3 phase    class points update from the ping buffer into the pong buffer, the others copy through
 //   n := f_n (pointer swap)
 // The update kNN list (k_u = 8) is the first k_u columns of the k list: same query positions, same snapshot.
+//
+// Spatial slabs (multi-GPU): the grid holds a rank's own points plus a halo of other ranks' snapshot points.  Only
+// the ACTIVE rows (pcd_denoiser_set_rows) are queried and updated; the halo rows' state is written by the caller's
+// exchange between stages (pcd_denoiser_pack/unpack), and the global flat centre / delta reductions are exposed as
+// separate stages so the caller can all-reduce them (pcd_denoiser_stage).  pcd_denoiser_iterate is the same stage
+// sequence with no exchange.
 #include <vector>
 
 #include "pcd_knn.h"
@@ -51,38 +57,72 @@ __global__ void k_store(const float4* __restrict__ pos_s, const float4* __restri
     if (edge) { const float4 p = edge_s[r]; edge[3 * i] = p.x; edge[3 * i + 1] = p.y; edge[3 * i + 2] = p.z; }
 }
 
+// Active-row view: thread t works on row rows[t] (sorted order), or on row t when rows is null.
+struct RowMap {
+    const int32_t* rows;
+    int64_t nq;
+    PCD_DEV int64_t operator()(int64_t t) const { return rows ? (int64_t)rows[t] : t; }
+};
+
+// Local snapshot coverage: the kNN of a query is exact when its k-ball lies inside this box (spatial slabs:
+// the slab widened by the halo).  Disabled when lo > hi on axis 0.
+struct Cover {
+    float lo[3], hi[3];
+    PCD_DEV bool holds(Vec3 q, float d2) const {
+        if (lo[0] > hi[0]) return true;
+        const float r = sqrtf(d2) * 1.000001f + 1e-30f;
+        return q.x - r >= lo[0] && q.x + r <= hi[0] && q.y - r >= lo[1] && q.y + r <= hi[1] && q.z - r >= lo[2] &&
+               q.z + r <= hi[2];
+    }
+};
+
 // K1: kNN + NVT1 + VU smoothing.
-// SEED (iterations after the first): the largest key of last
-// iteration's list (kstore distinct snapshot points) caps the acceptance threshold from the first candidate on.
+// SEED (iterations after the first): the largest key of last iteration's list (kstore distinct snapshot points),
+// re-keyed at the current position, caps the acceptance threshold from the first candidate on, and the capped
+// search (LDS append + one sorted drain) replaces per-candidate inserts.
+// err bits: 1 = invalid list entry (internal error), 2 = a k-ball leaves the local snapshot's coverage box.
+static constexpr int kCapRows = 48;  // LDS rows per lane: 48 KB per 256-thread block
 template <int K, bool SEED>
 __global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __restrict__ pos,
-                                                   const float4* __restrict__ nrm, int64_t N, int k, int kstore,
-                                                   float rho, float tau, float damp, int32_t* __restrict__ idx,
-                                                   float4* __restrict__ fn, int* __restrict__ err) {
-    const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    if (i >= N) return;
+                                                   const float4* __restrict__ nrm, int64_t N, RowMap rm, int k,
+                                                   int kstore, float rho, float tau, float damp, Cover cov,
+                                                   int32_t* __restrict__ idx, float4* __restrict__ fn,
+                                                   int* __restrict__ err) {
+    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (t0 >= rm.nq) return;
+    const int64_t i = rm(t0);
     const float4 p4 = pos[i];
     const Vec3 vi = v3(p4.x, p4.y, p4.z);
     TopK<K> tk;
     unsigned long long cap = kInfKey;
     if constexpr (SEED) {           // max key of last iteration's list >= this iteration's kstore-th key
+        // all list rows first (K loads in flight), then their points; columns >= kstore re-read column 0
+        uint32_t sd[K];
+#pragma unroll
+        for (int t = 0; t < K; ++t) sd[t] = (uint32_t)idx[(int64_t)(t < kstore ? t : 0) * N + i];
         cap = 0ull;
 #pragma unroll
         for (int t = 0; t < K; ++t) {
-            if (t < kstore) {
-                const uint32_t sd = (uint32_t)idx[(int64_t)t * N + i];
-                const unsigned long long c = cand_key<false>(vi, g.pts[sd], sd);
-                cap = c > cap ? c : cap;
-            }
+            const unsigned long long c = cand_key<false>(vi, g.pts[sd[t]], sd[t]);
+            cap = c > cap ? c : cap;
         }
         cap += 1ull;                 // acceptance is `key < cap`: keep the seed list's own largest key
     }
-    knn_search<K, false>(g, vi, tk, cap);
+    if constexpr (SEED && K <= 32) {
+        __shared__ uint32_t s_buf[kCapRows * kCapStride];
+        knn_search_capped<K, kCapRows>(g, vi, tk, cap, s_buf + threadIdx.x);
+    } else if constexpr (SEED) {
+        knn_search<K, false>(g, vi, tk, cap);
+    } else {
+        knn_search<K, false>(g, vi, tk);
+    }
     int l[K];
     bool bad = false;
+    float dk = 0.f;                  // d² of the kstore-th neighbour (static select: no dynamic register index)
 #pragma unroll
     for (int t = 0; t < K; ++t) {
         l[t] = tk.idx(t);
+        if (t == kstore - 1) dk = tk.d2(t);
         if (t < kstore) {
             // a list entry that is not a point would be an internal error: record it, never fault on it
             if ((uint32_t)l[t] >= (uint32_t)N) { bad = true; l[t] = (int)i; }
@@ -90,6 +130,7 @@ __global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __re
         }
     }
     if (bad) atomicOr(err, 1);
+    if (!cov.holds(vi, dk)) atomicOr(err, 2);
     const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho);
     float w[3], V[3][3];
     eigh3(T, w, V);
@@ -100,10 +141,12 @@ __global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __re
 // K2: NVT2 on f_n -> classes + edge vectors.
 template <int K>
 __global__ __launch_bounds__(256) void k_nvt2(const float4* __restrict__ pos, const float4* __restrict__ fn,
-                                               const int32_t* __restrict__ idx, int64_t N, int k, float rho,
-                                               float scale, uint8_t* __restrict__ cls, float4* __restrict__ edge) {
-    const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    if (i >= N) return;
+                                               const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
+                                               float rho, float scale, uint8_t* __restrict__ cls,
+                                               float4* __restrict__ edge) {
+    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (t0 >= rm.nq) return;
+    const int64_t i = rm(t0);
     const float4 p4 = pos[i];
     const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{fn}, v3(p4.x, p4.y, p4.z), k, ColNb{idx, N, i}, rho);
     float w[3], V[3][3];
@@ -114,13 +157,15 @@ __global__ __launch_bounds__(256) void k_nvt2(const float4* __restrict__ pos, co
 
 struct RedC { double sx, sy, sz, cnt; };
 
-__global__ void k_class_rows_sum(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N, int ku,
-                                 const uint8_t* __restrict__ cls, int c, RedC* __restrict__ part) {
+// Flat-phase centre, pass 1: per-block f64 partial sums of the k_u neighbour rows of the class-c points.
+__global__ void k_class_rows_sum(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N, RowMap rm,
+                                 int ku, const uint8_t* __restrict__ cls, int c, RedC* __restrict__ part) {
     double sx = 0, sy = 0, sz = 0, cnt = 0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < rm.nq; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = rm(t);
         if (cls[i] != c) continue;
-        for (int t = 0; t < ku; ++t) {
-            const float4 v = pos[idx[(int64_t)t * N + i]];
+        for (int u = 0; u < ku; ++u) {
+            const float4 v = pos[idx[(int64_t)u * N + i]];
             sx += v.x; sy += v.y; sz += v.z;
         }
         cnt += ku;
@@ -136,7 +181,8 @@ __global__ void k_class_rows_sum(const float4* __restrict__ pos, const int32_t* 
     if (threadIdx.x == 0) part[blockIdx.x] = RedC{s[0][0], s[1][0], s[2][0], s[3][0]};
 }
 
-__global__ void k_class_centre(const RedC* __restrict__ part, int np, float* __restrict__ g) {
+// pass 2: the partials -> (Σx, Σy, Σz, count) in f64 (what a multi-rank caller all-reduces).
+__global__ void k_part_reduce(const RedC* __restrict__ part, int np, double* __restrict__ red) {
     __shared__ double s[4][256];
     double a[4] = {0, 0, 0, 0};
     for (int b = threadIdx.x; b < np; b += blockDim.x) { a[0] += part[b].sx; a[1] += part[b].sy; a[2] += part[b].sz; a[3] += part[b].cnt; }
@@ -147,23 +193,30 @@ __global__ void k_class_centre(const RedC* __restrict__ part, int np, float* __r
             for (int q = 0; q < 4; ++q) s[q][threadIdx.x] += s[q][threadIdx.x + w];
         __syncthreads();
     }
+    if (threadIdx.x == 0) for (int q = 0; q < 4; ++q) red[q] = s[q][0];
+}
+
+// pass 3: centre = Σ / count (the reference's f32 mean over all E rows, Denoiser.py:106), delta reset.
+__global__ void k_centre(const double* __restrict__ red, float* __restrict__ g) {
     if (threadIdx.x == 0) {
-        const double c = s[3][0];
-        g[0] = (float)(s[0][0] / c);
-        g[1] = (float)(s[1][0] / c);
-        g[2] = (float)(s[2][0] / c);
+        const double c = red[3];
+        g[0] = (float)(red[0] / c);
+        g[1] = (float)(red[1] / c);
+        g[2] = (float)(red[2] / c);
         reinterpret_cast<unsigned int*>(g)[3] = 0u;
     }
 }
 
+// pass 4: delta = max ||v_j - centre|| over the same rows (Denoiser.py:107), atomicMax on the f32 bits.
 __global__ void k_class_rows_maxdist(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N,
-                                     int ku, const uint8_t* __restrict__ cls, int c, float* __restrict__ g) {
+                                     RowMap rm, int ku, const uint8_t* __restrict__ cls, int c, float* __restrict__ g) {
     const Vec3 ctr = v3(g[0], g[1], g[2]);
     float mx = 0.f;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < rm.nq; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = rm(t);
         if (cls[i] != c) continue;
-        for (int t = 0; t < ku; ++t) {
-            const float4 v = pos[idx[(int64_t)t * N + i]];
+        for (int u = 0; u < ku; ++u) {
+            const float4 v = pos[idx[(int64_t)u * N + i]];
             mx = fmaxf(mx, sqrtf(sq3(v3(v.x, v.y, v.z) - ctr)));
         }
     }
@@ -171,15 +224,20 @@ __global__ void k_class_rows_maxdist(const float4* __restrict__ pos, const int32
     if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(g) + 3, __float_as_uint(mx));
 }
 
-// K3: one Gauss-Seidel phase: points of class c move (reading pin), all others copy through to pout.
+__global__ void k_copy_delta(const float* __restrict__ from, float* __restrict__ to) {
+    if (threadIdx.x == 0) *to = *from;
+}
+
+// K3: one Gauss-Seidel phase: active points of class c move (reading pin), other active points copy through.
 template <int KIND>
 __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, float4* __restrict__ pout,
                                                 const float4* __restrict__ fn, const float4* __restrict__ edge,
-                                                const int32_t* __restrict__ idx, int64_t N, int ku,
+                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int ku,
                                                 const uint8_t* __restrict__ cls, int c, const float* __restrict__ g,
                                                 float d, float alpha) {
-    const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    if (i >= N) return;
+    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (t0 >= rm.nq) return;
+    const int64_t i = rm(t0);
     const float4 p4 = pin[i];
     if (cls[i] != c) { pout[i] = p4; return; }
     const Vec3 vi = v3(p4.x, p4.y, p4.z);
@@ -195,6 +253,16 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     store4(pout, i, o);
 }
 
+// halo exchange: rows of one state field <-> a packed float4 buffer
+__global__ void k_pack(const float4* __restrict__ f, const int32_t* __restrict__ rows, int64_t n, float4* __restrict__ out) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t < n) out[t] = f[rows[t]];
+}
+__global__ void k_unpack(float4* __restrict__ f, const int32_t* __restrict__ rows, int64_t n, const float4* __restrict__ in) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t < n) f[rows[t]] = in[t];
+}
+
 }  // namespace pcd
 
 using namespace pcd;
@@ -208,17 +276,151 @@ struct pcd_denoiser {
     int32_t* idx = nullptr;
     uint8_t* cls = nullptr;
     RedC* part = nullptr;
+    double* red = nullptr;        // 4 doubles per phase: (Σx, Σy, Σz, count) of the global reductions
     float* gscal = nullptr;       // 4 floats per phase: centre xyz, delta bits
-    int* err = nullptr;           // device error word (invalid kNN entries), checked by store()
+    int* err = nullptr;           // device error word (see k_knn_nvt1), checked by store() / check()
+    const int32_t* rows = nullptr;  // active rows (sorted order), or null = all rows
+    int64_t n_rows = 0;
+    Cover cov{{1.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};  // disabled
     int seed_cols = 0;            // columns of idx holding a valid kNN list of the snapshot (0: none yet)
     bool seeding = false;         // use the stored list as an acceptance cap (pcd_denoiser_set_seeding)
     bool loaded = false, iterated = false;
     bool timing = false;
     std::vector<hipEvent_t> ev;
     std::vector<float> ms;
+    RowMap rowmap() const { return RowMap{rows, rows ? n_rows : n}; }
 };
 
 static const int kNumPart = 1024;
+
+static int check_params(const pcd_denoiser* dn, const pcd_denoise_params* p) {
+    PCD_CHECK_ARG(dn && p, "null argument");
+    PCD_CHECK_ARG(dn->loaded, "pcd_denoiser_load must be called first");
+    PCD_CHECK_ARG(p->k >= 1 && p->k_update >= 1, "k, k_update must be >= 1");
+    PCD_CHECK_ARG(std::max(p->k, p->k_update) <= dn->kcap, "k / k_update exceed the k_max given at create");
+    PCD_CHECK_ARG(std::max(p->k, p->k_update) <= dn->n, "k exceeds the number of points");
+    PCD_CHECK_ARG(p->nphases >= 0 && p->nphases <= 3, "nphases must be 0..3");
+    for (int ph = 0; ph < p->nphases; ++ph) {
+        PCD_CHECK_ARG(p->phase_class[ph] >= 0 && p->phase_class[ph] <= 2, "phase class must be 0, 1 or 2");
+        PCD_CHECK_ARG(p->phase_kind[ph] >= PCD_STEP_FLAT && p->phase_kind[ph] <= PCD_STEP_DUMMY, "bad phase kind");
+    }
+    return PCD_OK;
+}
+
+static int list_cap(const pcd_denoise_params* p) {
+    const int kstore = std::max(p->k, p->k_update);
+    return kstore <= 8 ? 8 : kstore <= 16 ? 16 : kstore <= 32 ? 32 : 64;
+}
+
+static bool phase_is_global(const pcd_denoise_params* p, int ph) {
+    return p->phase_kind[ph] == PCD_STEP_FLAT || p->phase_kind[ph] == PCD_STEP_NEW;
+}
+
+static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t st) {
+    const int64_t N = dn->n;
+    const RowMap rm = dn->rowmap();
+    if (rm.nq == 0) return PCD_OK;
+    const int kstore = std::max(p->k, p->k_update);
+    const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
+    const GridView gv = dn->g->view;
+    float4* P = dn->pos[dn->cur];
+    const bool seed = dn->seeding && dn->seed_cols >= kstore;
+#define PCD_K1(C)                                                                                                      \
+    case C:                                                                                                            \
+        if (seed) hipLaunchKernelGGL((k_knn_nvt1<C, true>), grd, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore, p->rho, p->tau, p->damp, dn->cov, dn->idx, dn->fn, dn->err); \
+        else hipLaunchKernelGGL((k_knn_nvt1<C, false>), grd, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore, p->rho, p->tau, p->damp, dn->cov, dn->idx, dn->fn, dn->err); \
+        break;
+    switch (list_cap(p)) {
+        PCD_K1(8) PCD_K1(16) PCD_K1(32) PCD_K1(64)
+        default: return fail(PCD_ERR_ARG, "unsupported k");
+    }
+#undef PCD_K1
+    PCD_LAUNCH_CHECK();
+    dn->seed_cols = kstore;
+    return PCD_OK;
+}
+
+static int stage_k2(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t st) {
+    const RowMap rm = dn->rowmap();
+    if (rm.nq == 0) return PCD_OK;
+    const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
+    float4* P = dn->pos[dn->cur];
+#define PCD_K2(C) \
+    case C: hipLaunchKernelGGL(k_nvt2<C>, grd, blk, 0, st, P, dn->fn, dn->idx, dn->n, rm, p->k, p->rho, p->class_scale, dn->cls, dn->edge); break;
+    switch (list_cap(p)) {
+        PCD_K2(8) PCD_K2(16) PCD_K2(32) PCD_K2(64)
+        default: return fail(PCD_ERR_ARG, "unsupported k");
+    }
+#undef PCD_K2
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+// local (Σx, Σy, Σz, count) of phase ph -> red4 (device)
+static int stage_sum(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, double* red4, hipStream_t st) {
+    const int c = p->phase_class[ph];
+    hipLaunchKernelGGL(k_class_rows_sum, dim3(kNumPart), dim3(256), 0, st, dn->pos[dn->cur], dn->idx, dn->n,
+                       dn->rowmap(), p->k_update, dn->cls, c, dn->part);
+    hipLaunchKernelGGL(k_part_reduce, dim3(1), dim3(256), 0, st, dn->part, kNumPart, red4);
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+static int stage_centre(pcd_denoiser* dn, int ph, const double* red4, hipStream_t st) {
+    hipLaunchKernelGGL(k_centre, dim3(1), dim3(64), 0, st, red4, dn->gscal + 4 * ph);
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+// local max distance of phase ph -> gscal delta (and *red1 when given)
+static int stage_maxdist(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, float* red1, hipStream_t st) {
+    float* gs = dn->gscal + 4 * ph;
+    hipLaunchKernelGGL(k_class_rows_maxdist, dim3(kNumPart), dim3(256), 0, st, dn->pos[dn->cur], dn->idx, dn->n,
+                       dn->rowmap(), p->k_update, dn->cls, p->phase_class[ph], gs);
+    if (red1) hipLaunchKernelGGL(k_copy_delta, dim3(1), dim3(64), 0, st, gs + 3, red1);
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, const float* red1, hipStream_t st) {
+    const RowMap rm = dn->rowmap();
+    float* gs = dn->gscal + 4 * ph;
+    if (red1) hipLaunchKernelGGL(k_copy_delta, dim3(1), dim3(64), 0, st, red1, gs + 3);
+    const int kind = p->phase_kind[ph], c = p->phase_class[ph];
+    const float a = p->phase_alpha[ph];
+    float4* pin = dn->pos[dn->cur];
+    float4* pout = dn->pos[dn->cur ^ 1];
+    if (rm.nq > 0) {
+        const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
+#define PCD_PH(KD) hipLaunchKernelGGL(k_phase<KD>, grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, dn->n, rm, p->k_update, dn->cls, c, gs, p->d, a)
+        switch (kind) {
+            case PCD_STEP_FLAT: PCD_PH(PCD_STEP_FLAT); break;
+            case PCD_STEP_EDGE: PCD_PH(PCD_STEP_EDGE); break;
+            case PCD_STEP_FEATURE: PCD_PH(PCD_STEP_FEATURE); break;
+            case PCD_STEP_CORNER: PCD_PH(PCD_STEP_CORNER); break;
+            case PCD_STEP_NEW: PCD_PH(PCD_STEP_NEW); break;
+            default: PCD_PH(PCD_STEP_DUMMY); break;
+        }
+#undef PCD_PH
+        PCD_LAUNCH_CHECK();
+    }
+    dn->cur ^= 1;
+    return PCD_OK;
+}
+
+static void stage_finish(pcd_denoiser* dn) {
+    std::swap(dn->nrm, dn->fn);   // graph.n = f_n  (Processor.py:139)
+    dn->iterated = true;
+}
+
+static float4* field_ptr(pcd_denoiser* dn, int field) {
+    switch (field) {
+        case PCD_FIELD_POS: return dn->pos[dn->cur];
+        case PCD_FIELD_NRM: return dn->nrm;
+        case PCD_FIELD_FN: return dn->fn;
+        default: return nullptr;
+    }
+}
 
 extern "C" {
 
@@ -230,8 +432,6 @@ int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out) {
     pcd_denoiser* dn = new pcd_denoiser();
     dn->g = g;
     dn->n = g->n;
-    int cap = knn_cap(k_max);
-    if (cap < 8) cap = 8;
     dn->kcap = k_max;
     const int64_t N = g->n;
     bool ok = hipMalloc(&dn->pos[0], N * sizeof(float4)) == hipSuccess &&
@@ -242,8 +442,10 @@ int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out) {
               hipMalloc(&dn->idx, (int64_t)k_max * N * sizeof(int32_t)) == hipSuccess &&
               hipMalloc(&dn->cls, N) == hipSuccess &&
               hipMalloc(&dn->part, kNumPart * sizeof(RedC)) == hipSuccess &&
+              hipMalloc(&dn->red, 16 * sizeof(double)) == hipSuccess &&
               hipMalloc(&dn->gscal, 16 * sizeof(float)) == hipSuccess &&
-              hipMalloc(&dn->err, sizeof(int)) == hipSuccess && hipMemset(dn->err, 0, sizeof(int)) == hipSuccess;
+              hipMalloc(&dn->err, sizeof(int)) == hipSuccess && hipMemset(dn->err, 0, sizeof(int)) == hipSuccess &&
+              hipMemset(dn->cls, 0xFF, N) == hipSuccess;
     if (!ok) {
         pcd_denoiser_destroy(dn);
         return fail(PCD_ERR_OOM, "pcd_denoiser_create: device allocation");
@@ -254,9 +456,9 @@ int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out) {
 
 int pcd_denoiser_destroy(pcd_denoiser* dn) {
     if (!dn) return PCD_OK;
-    (void)(void)hipFree(dn->pos[0]); (void)hipFree(dn->pos[1]); (void)hipFree(dn->nrm); (void)hipFree(dn->fn); (void)hipFree(dn->edge);
-    (void)(void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part); (void)hipFree(dn->gscal);
-    (void)hipFree(dn->err);
+    (void)hipFree(dn->pos[0]); (void)hipFree(dn->pos[1]); (void)hipFree(dn->nrm); (void)hipFree(dn->fn);
+    (void)hipFree(dn->edge); (void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part);
+    (void)hipFree(dn->red); (void)hipFree(dn->gscal); (void)hipFree(dn->err);
     for (auto e : dn->ev) (void)hipEventDestroy(e);
     delete dn;
     return PCD_OK;
@@ -270,6 +472,85 @@ int pcd_denoiser_load(pcd_denoiser* dn, const float* pos, const float* n, void* 
     dn->cur = 0;
     dn->loaded = true;
     dn->iterated = false;
+    dn->seed_cols = 0;
+    return PCD_OK;
+}
+
+int pcd_denoiser_set_rows(pcd_denoiser* dn, const int32_t* rows, int64_t n_rows) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    PCD_CHECK_ARG(rows != nullptr || n_rows == 0, "rows is null");
+    PCD_CHECK_ARG(n_rows >= 0 && n_rows <= dn->n, "n_rows out of range");
+    dn->rows = rows;
+    dn->n_rows = rows ? n_rows : 0;
+    return PCD_OK;
+}
+
+int pcd_denoiser_set_coverage(pcd_denoiser* dn, const float* lo3, const float* hi3) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    if (!lo3 || !hi3) {
+        dn->cov = Cover{{1.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+        return PCD_OK;
+    }
+    for (int a = 0; a < 3; ++a) {
+        PCD_CHECK_ARG(!(lo3[a] > hi3[a]), "coverage box has lo > hi");
+        dn->cov.lo[a] = lo3[a];
+        dn->cov.hi[a] = hi3[a];
+    }
+    return PCD_OK;
+}
+
+int pcd_denoiser_pack(pcd_denoiser* dn, int field, const int32_t* rows, int64_t n, float* out4, void* stream) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    float4* f = field_ptr(dn, field);
+    PCD_CHECK_ARG(f != nullptr, "bad field");
+    PCD_CHECK_ARG(n == 0 || (rows && out4), "null rows / buffer");
+    if (n == 0) return PCD_OK;
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, as_stream(stream), f, rows, n,
+                       reinterpret_cast<float4*>(out4));
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+int pcd_denoiser_unpack(pcd_denoiser* dn, int field, const int32_t* rows, int64_t n, const float* in4, void* stream) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    float4* f = field_ptr(dn, field);
+    PCD_CHECK_ARG(f != nullptr, "bad field");
+    PCD_CHECK_ARG(n == 0 || (rows && in4), "null rows / buffer");
+    if (n == 0) return PCD_OK;
+    hipLaunchKernelGGL(k_unpack, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, as_stream(stream), f, rows, n,
+                       reinterpret_cast<const float4*>(in4));
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+int pcd_denoiser_stage(pcd_denoiser* dn, const pcd_denoise_params* p, int stage, int phase, void* red,
+                       void* stream) {
+    const int rc = check_params(dn, p);
+    if (rc != PCD_OK) return rc;
+    PCD_CHECK_ARG(stage >= PCD_STAGE_KNN_NVT1 && stage <= PCD_STAGE_FINISH, "bad stage");
+    const bool ph_stage = stage >= PCD_STAGE_PHASE_SUM && stage <= PCD_STAGE_PHASE_APPLY;
+    PCD_CHECK_ARG(!ph_stage || (phase >= 0 && phase < p->nphases), "phase out of range");
+    PCD_CHECK_ARG(!(stage == PCD_STAGE_PHASE_SUM || stage == PCD_STAGE_PHASE_CENTRE) || red, "red is null");
+    hipStream_t st = as_stream(stream);
+    switch (stage) {
+        case PCD_STAGE_KNN_NVT1: return stage_k1(dn, p, st);
+        case PCD_STAGE_NVT2: return stage_k2(dn, p, st);
+        case PCD_STAGE_PHASE_SUM: return stage_sum(dn, p, phase, static_cast<double*>(red), st);
+        case PCD_STAGE_PHASE_CENTRE: return stage_centre(dn, phase, static_cast<const double*>(red), st);
+        case PCD_STAGE_PHASE_MAXDIST: return stage_maxdist(dn, p, phase, static_cast<float*>(red), st);
+        case PCD_STAGE_PHASE_APPLY: return stage_apply(dn, p, phase, static_cast<const float*>(red), st);
+        default: stage_finish(dn); return PCD_OK;
+    }
+}
+
+int pcd_denoiser_check(pcd_denoiser* dn, void* stream) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    int err = 0;
+    PCD_HIP(hipMemcpyAsync(&err, dn->err, sizeof(int), hipMemcpyDeviceToHost, as_stream(stream)));
+    PCD_HIP(hipStreamSynchronize(as_stream(stream)));
+    if (err & 1) return fail(PCD_ERR_STATE, "pcd_denoiser: the kNN kernel produced an invalid neighbour index");
+    if (err & 2)
+        return fail(PCD_ERR_STATE, "pcd_denoiser: a k-neighbourhood reaches past the local snapshot (halo too thin)");
     return PCD_OK;
 }
 
@@ -311,80 +592,31 @@ int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n
 }
 
 int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iterations, void* stream) {
-    PCD_CHECK_ARG(dn && p, "null argument");
-    PCD_CHECK_ARG(dn->loaded, "pcd_denoiser_load must be called first");
-    PCD_CHECK_ARG(p->k >= 1 && p->k_update >= 1, "k, k_update must be >= 1");
-    PCD_CHECK_ARG(std::max(p->k, p->k_update) <= dn->kcap, "k / k_update exceed the k_max given at create");
-    PCD_CHECK_ARG(std::max(p->k, p->k_update) <= dn->n, "k exceeds the number of points");
-    PCD_CHECK_ARG(p->nphases >= 0 && p->nphases <= 3, "nphases must be 0..3");
-    for (int ph = 0; ph < p->nphases; ++ph) {
-        PCD_CHECK_ARG(p->phase_class[ph] >= 0 && p->phase_class[ph] <= 2, "phase class must be 0, 1 or 2");
-        PCD_CHECK_ARG(p->phase_kind[ph] >= PCD_STEP_FLAT && p->phase_kind[ph] <= PCD_STEP_DUMMY, "bad phase kind");
-    }
+    int rc = check_params(dn, p);
+    if (rc != PCD_OK) return rc;
     hipStream_t st = as_stream(stream);
-    const int64_t N = dn->n;
-    const int kstore = std::max(p->k, p->k_update);
-    const int cap = kstore <= 8 ? 8 : kstore <= 16 ? 16 : kstore <= 32 ? 32 : 64;
-    const dim3 blk(256), grd((unsigned)cdiv(N, 256));
-    const GridView gv = dn->g->view;
     for (int it = 0; it < iterations; ++it) {
         const bool rec = dn->timing && it == iterations - 1;
         if (rec) PCD_HIP(hipEventRecord(dn->ev[0], st));
-        float4* P = dn->pos[dn->cur];
-        const bool seed = dn->seeding && dn->seed_cols >= kstore;
-#define PCD_K1(C) \
-    case C:                                                                                                          \
-        if (seed) hipLaunchKernelGGL((k_knn_nvt1<C, true>), grd, blk, 0, st, gv, P, dn->nrm, N, p->k, kstore, p->rho, p->tau, p->damp, dn->idx, dn->fn, dn->err); \
-        else hipLaunchKernelGGL((k_knn_nvt1<C, false>), grd, blk, 0, st, gv, P, dn->nrm, N, p->k, kstore, p->rho, p->tau, p->damp, dn->idx, dn->fn, dn->err); \
-        break;
-        switch (cap) {
-            PCD_K1(8) PCD_K1(16) PCD_K1(32) PCD_K1(64)
-            default: return fail(PCD_ERR_ARG, "unsupported k");
-        }
-#undef PCD_K1
-        PCD_LAUNCH_CHECK();
-        dn->seed_cols = kstore;
+        if ((rc = stage_k1(dn, p, st)) != PCD_OK) return rc;
         if (rec) PCD_HIP(hipEventRecord(dn->ev[1], st));
-#define PCD_K2(C) \
-    case C: hipLaunchKernelGGL(k_nvt2<C>, grd, blk, 0, st, P, dn->fn, dn->idx, N, p->k, p->rho, p->class_scale, dn->cls, dn->edge); break;
-        switch (cap) {
-            PCD_K2(8) PCD_K2(16) PCD_K2(32) PCD_K2(64)
-            default: return fail(PCD_ERR_ARG, "unsupported k");
-        }
-#undef PCD_K2
-        PCD_LAUNCH_CHECK();
+        if ((rc = stage_k2(dn, p, st)) != PCD_OK) return rc;
         if (rec) PCD_HIP(hipEventRecord(dn->ev[2], st));
         for (int ph = 0; ph < p->nphases; ++ph) {
-            const int kind = p->phase_kind[ph], c = p->phase_class[ph];
-            float* gs = dn->gscal + 4 * ph;
-            float4* pin = dn->pos[dn->cur];
-            float4* pout = dn->pos[dn->cur ^ 1];
-            if (kind == PCD_STEP_FLAT || kind == PCD_STEP_NEW) {
-                hipLaunchKernelGGL(k_class_rows_sum, dim3(kNumPart), blk, 0, st, pin, dn->idx, N, p->k_update, dn->cls, c, dn->part);
-                hipLaunchKernelGGL(k_class_centre, dim3(1), blk, 0, st, dn->part, kNumPart, gs);
-                hipLaunchKernelGGL(k_class_rows_maxdist, dim3(kNumPart), blk, 0, st, pin, dn->idx, N, p->k_update, dn->cls, c, gs);
+            if (phase_is_global(p, ph)) {
+                double* red4 = dn->red + 4 * ph;
+                if ((rc = stage_sum(dn, p, ph, red4, st)) != PCD_OK) return rc;
+                if ((rc = stage_centre(dn, ph, red4, st)) != PCD_OK) return rc;
+                if ((rc = stage_maxdist(dn, p, ph, nullptr, st)) != PCD_OK) return rc;
             }
-            const float a = p->phase_alpha[ph];
-#define PCD_PH(KD) hipLaunchKernelGGL(k_phase<KD>, grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, N, p->k_update, dn->cls, c, gs, p->d, a)
-            switch (kind) {
-                case PCD_STEP_FLAT: PCD_PH(PCD_STEP_FLAT); break;
-                case PCD_STEP_EDGE: PCD_PH(PCD_STEP_EDGE); break;
-                case PCD_STEP_FEATURE: PCD_PH(PCD_STEP_FEATURE); break;
-                case PCD_STEP_CORNER: PCD_PH(PCD_STEP_CORNER); break;
-                case PCD_STEP_NEW: PCD_PH(PCD_STEP_NEW); break;
-                default: PCD_PH(PCD_STEP_DUMMY); break;
-            }
-#undef PCD_PH
-            PCD_LAUNCH_CHECK();
-            dn->cur ^= 1;
+            if ((rc = stage_apply(dn, p, ph, nullptr, st)) != PCD_OK) return rc;
             if (rec) PCD_HIP(hipEventRecord(dn->ev[3 + ph], st));
         }
         if (rec)
             for (int ph = p->nphases; ph < 3; ++ph) PCD_HIP(hipEventRecord(dn->ev[3 + ph], st));
-        std::swap(dn->nrm, dn->fn);   // graph.n = f_n  (Processor.py:139)
+        stage_finish(dn);
         if (rec) PCD_HIP(hipEventRecord(dn->ev[6], st));
         if (rec) PCD_HIP(hipEventRecord(dn->ev[7], st));
-        dn->iterated = true;
     }
     return PCD_OK;
 }
@@ -397,11 +629,7 @@ int pcd_denoiser_store(pcd_denoiser* dn, float* pos, float* n, int64_t* classes,
     hipLaunchKernelGGL(k_store, dim3((unsigned)cdiv(dn->n, 256)), dim3(256), 0, as_stream(stream), dn->pos[dn->cur],
                        dn->nrm, dn->cls, dn->edge, dn->g->perm, dn->n, pos, n, classes, edge_vectors);
     PCD_LAUNCH_CHECK();
-    int err = 0;
-    PCD_HIP(hipMemcpyAsync(&err, dn->err, sizeof(int), hipMemcpyDeviceToHost, as_stream(stream)));
-    PCD_HIP(hipStreamSynchronize(as_stream(stream)));
-    if (err) return fail(PCD_ERR_STATE, "pcd_denoiser: the kNN kernel produced an invalid neighbour index");
-    return PCD_OK;
+    return pcd_denoiser_check(dn, stream);
 }
 
 }  // extern "C"

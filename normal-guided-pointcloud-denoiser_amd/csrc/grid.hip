@@ -204,21 +204,12 @@ const char* pcd_last_error(void) { return g_last_error.c_str(); }
 int pcd_version(void) { return 1; }
 int pcd_max_k(void) { return 64; }
 
-int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, void* stream, pcd_grid** out) {
-    PCD_CHECK_ARG(out != nullptr, "out is null");
-    *out = nullptr;
-    PCD_CHECK_ARG(xyz != nullptr && n > 0, "empty point set");
-    PCD_CHECK_ARG(n < (int64_t)INT32_MAX, "more than 2^31-1 points in one grid");
-    hipStream_t st = as_stream(stream);
-    pcd_grid* g = new pcd_grid();
-    g->n = n;
-    PCD_HIP(hipGetDevice(&g->device));
-    auto cleanup = [&]() { pcd_grid_destroy(g); };
-
-    // bbox
+// bbox + cell edge of a point set (the part of the build that fixes the cell lattice).
+static int grid_lattice(const float* xyz, int64_t n, int k_hint, float cell, hipStream_t st, float mn[3], float mx[3],
+                        float& h_out) {
     const int nbb = 512;
     float* part = nullptr;
-    if (hipMalloc(&part, nbb * 6 * sizeof(float)) != hipSuccess) { cleanup(); return fail(PCD_ERR_OOM, "bbox"); }
+    if (hipMalloc(&part, nbb * 6 * sizeof(float)) != hipSuccess) return fail(PCD_ERR_OOM, "bbox");
     hipLaunchKernelGGL(k_bbox, dim3(nbb), dim3(256), 0, st, xyz, n, part);
     std::vector<float> hp(nbb * 6);
     (void)hipMemcpyAsync(hp.data(), part, nbb * 6 * sizeof(float), hipMemcpyDeviceToHost, st);
@@ -226,25 +217,61 @@ int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, void* st
     const int64_t S = std::min<int64_t>(n, 65536);
     const int64_t stride = n / S;
     float* dsmp = nullptr;
-    if (hipMalloc(&dsmp, S * 3 * sizeof(float)) != hipSuccess) { (void)hipFree(part); cleanup(); return fail(PCD_ERR_OOM, "sample"); }
+    if (hipMalloc(&dsmp, S * 3 * sizeof(float)) != hipSuccess) { (void)hipFree(part); return fail(PCD_ERR_OOM, "sample"); }
     hipLaunchKernelGGL(k_sample, dim3((unsigned)cdiv(S, 256)), dim3(256), 0, st, xyz, n, stride, S, dsmp);
     std::vector<float> smp(S * 3);
     (void)hipMemcpyAsync(smp.data(), dsmp, S * 3 * sizeof(float), hipMemcpyDeviceToHost, st);
     hipError_t e = hipStreamSynchronize(st);
     (void)hipFree(part);
     (void)hipFree(dsmp);
-    if (e != hipSuccess) { cleanup(); return fail(PCD_ERR_HIP, std::string("grid bbox: ") + hipGetErrorString(e)); }
-    float mn[3], mx[3];
+    if (e != hipSuccess) return fail(PCD_ERR_HIP, std::string("grid bbox: ") + hipGetErrorString(e));
     for (int a = 0; a < 3; ++a) { mn[a] = 3.0e38f; mx[a] = -3.0e38f; }
     for (int b = 0; b < nbb; ++b)
         for (int a = 0; a < 3; ++a) { mn[a] = std::min(mn[a], hp[b * 6 + a]); mx[a] = std::max(mx[a], hp[b * 6 + 3 + a]); }
     for (int a = 0; a < 3; ++a)
-        if (!std::isfinite(mn[a]) || !std::isfinite(mx[a])) { cleanup(); return fail(PCD_ERR_ARG, "pcd_grid_build: non-finite coordinates"); }
+        if (!std::isfinite(mn[a]) || !std::isfinite(mx[a])) return fail(PCD_ERR_ARG, "pcd_grid_build: non-finite coordinates");
     float h = cell > 0 ? cell : choose_cell(smp, n, mn, mx, k_hint);
     for (int a = 0; a < 3; ++a) {
         const double dimd = std::floor(((double)mx[a] - mn[a]) / h) + 1.0;
         if (dimd >= 2097151.0) h = (float)(((double)mx[a] - mn[a]) / 2000000.0);
     }
+    h_out = h;
+    return PCD_OK;
+}
+
+int pcd_grid_params(const float* xyz, int64_t n, int k_hint, float cell, float* origin3, float* cell_out, void* stream) {
+    PCD_CHECK_ARG(xyz != nullptr && n > 0 && origin3 && cell_out, "null argument or empty point set");
+    float mn[3], mx[3], h;
+    const int rc = grid_lattice(xyz, n, k_hint, cell, as_stream(stream), mn, mx, h);
+    if (rc != PCD_OK) return rc;
+    for (int a = 0; a < 3; ++a) origin3[a] = mn[a];
+    *cell_out = h;
+    return PCD_OK;
+}
+
+int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, const float* origin3, void* stream,
+                   pcd_grid** out) {
+    PCD_CHECK_ARG(out != nullptr, "out is null");
+    *out = nullptr;
+    PCD_CHECK_ARG(xyz != nullptr && n > 0, "empty point set");
+    PCD_CHECK_ARG(n < (int64_t)INT32_MAX, "more than 2^31-1 points in one grid");
+    PCD_CHECK_ARG(!origin3 || cell > 0, "an explicit origin needs an explicit cell edge");
+    hipStream_t st = as_stream(stream);
+    float mn[3], mx[3], h;
+    int rc = grid_lattice(xyz, n, k_hint, cell, st, mn, mx, h);
+    if (rc != PCD_OK) return rc;
+    if (origin3) {
+        for (int a = 0; a < 3; ++a) {
+            PCD_CHECK_ARG(std::isfinite(origin3[a]) && origin3[a] <= mn[a], "origin must lie below every point");
+            mn[a] = origin3[a];
+            PCD_CHECK_ARG(std::floor(((double)mx[a] - mn[a]) / h) + 1.0 < 2097151.0, "origin/cell give more than 2^21 cells per axis");
+        }
+    }
+    pcd_grid* g = new pcd_grid();
+    g->n = n;
+    PCD_HIP(hipGetDevice(&g->device));
+    auto cleanup = [&]() { pcd_grid_destroy(g); };
+    hipError_t e;
     GridView& v = g->view;
     v.h = h;
     v.inv_h = 1.0f / h;

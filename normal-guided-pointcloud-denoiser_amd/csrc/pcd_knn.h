@@ -198,4 +198,195 @@ PCD_DEV void knn_search(const GridView& g, Vec3 q, TopK<K>& tk, unsigned long lo
     }
 }
 
+// ------------------------------------------------------------------ batched search (K >= 16)
+// The per-candidate sorted insert above costs ~6K VALU, and in SIMT it runs whenever ANY lane of the wave accepts,
+// i.e. on nearly every candidate.  The batched search flattens each lane's candidate stream across cell boundaries
+// so that batch slot b is a compile-time register for every lane: B candidate rows are resolved (cell walk + hash
+// probes), their B point loads issued together, the keys filtered against the k-th key, and a batch with any
+// survivor is merged into the sorted list with a fixed network: bitonic sort of the batch, elementwise min against
+// the list's tail (-> the K smallest of the union), then two bitonic merges.  ~100 compare-exchanges per batch
+// of B = 8, instead of up to B inserts of K compare-selects each.
+PCD_DEV void cswap(unsigned long long& a, unsigned long long& b) {
+    const bool sw = b < a;
+    const unsigned long long lo = sw ? b : a;
+    b = sw ? a : b;
+    a = lo;
+}
+
+// Bitonic merge of v[OFF .. OFF+N) (a bitonic sequence) into ascending (or descending) order, in place.
+template <int N, int OFF, int TOT, bool DESC = false>
+PCD_DEV void bitonic_merge(unsigned long long (&v)[TOT]) {
+#pragma unroll
+    for (int d = N / 2; d > 0; d >>= 1) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            if ((i & d) == 0) {
+                if (DESC) cswap(v[OFF + i + d], v[OFF + i]);
+                else cswap(v[OFF + i], v[OFF + i + d]);
+            }
+        }
+    }
+}
+
+// Ascending bitonic sort of v[0..N).
+template <int N>
+PCD_DEV void bitonic_sort(unsigned long long (&v)[N]) {
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (int stride = size / 2; stride > 0; stride >>= 1) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    if ((i & size) == 0) cswap(v[i], v[j]);
+                    else cswap(v[j], v[i]);
+                }
+            }
+        }
+    }
+}
+
+// key := the K smallest of key ∪ c, sorted (c: B keys, any order).  Elementwise min of the list's ascending tail
+// against the descending batch keeps exactly the K smallest of the union and leaves a bitonic tail; sorting that
+// tail DEscending makes the whole list bitonic (ascending head, descending tail), and one bitonic merge sorts it --
+// all in place, no copy of the list.
+template <int K, int B>
+PCD_DEV void topk_merge(TopK<K>& tk, unsigned long long (&c)[B]) {
+    static_assert(B <= K && (B & (B - 1)) == 0 && (K & (K - 1)) == 0, "power-of-two sizes");
+    bitonic_sort<B>(c);
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+        const unsigned long long x = c[B - 1 - i];
+        tk.key[K - B + i] = x < tk.key[K - B + i] ? x : tk.key[K - B + i];
+    }
+    if constexpr (K > B) {
+        bitonic_merge<B, K - B, K, true>(tk.key);
+        bitonic_merge<K, 0, K>(tk.key);
+    } else {
+        bitonic_merge<B, 0, K>(tk.key);
+    }
+}
+
+// ------------------------------------------------------------------ capped search (seeded iterations)
+// With an acceptance cap known to be >= the true k-th key and close to it (the previous iteration's list re-keyed
+// at the current position: median k, p99 ~1.4k keys below it on the denoise workload), a candidate below the cap
+// is only APPENDED to the lane's LDS row buffer (one ds_write; no SIMT-wide sorted insert).  The register list is
+// built once, at the end, by draining the buffer in chunks of 8 through topk_merge.  If a lane's buffer fills
+// (rare), the lane reduces it to its K best rows and tightens the cap to their k-th key + 1, so the list is never
+// live during the scan.  Exact for any cap >= the true k-th key.  Keys carry the snapshot rank (!ORIG).
+// buf = this lane's column of the block's [M][kCapStride] u32 row buffer.
+static constexpr int kCapStride = 256;
+
+template <int K, int M>
+PCD_DEV void cap_drain(const GridView& g, Vec3 q, TopK<K>& tk, const uint32_t* buf, int cnt) {
+    // unrolled over the (bounded) chunk count: the list stays in place, no loop-carried copy of it
+#pragma unroll
+    for (int base = 0; base < M; base += 8) {
+        if (__any(base < cnt)) {
+            unsigned long long c[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const bool ok = base + b < cnt;
+                const uint32_t r = ok ? buf[(base + b) * kCapStride] : 0u;
+                const float4 p = g.pts[r];
+                c[b] = ok ? cand_key<false>(q, p, r) : kInfKey;
+            }
+            topk_merge<K, 8>(tk, c);
+            PCD_KSTAT(tk, 4, 1);
+        }
+    }
+}
+
+template <int K, int M>
+struct CapState {
+    unsigned long long lim;  // acceptance cap: every key < lim is buffered
+    int cnt;                 // rows in the buffer
+    uint32_t* buf;
+#ifdef PCD_KNN_STATS
+    unsigned* stat;
+#endif
+    PCD_DEV float kth() const { return __uint_as_float((unsigned)(lim >> 32)); }
+};
+
+template <int K, int M>
+PCD_DEV void cap_overflow(const GridView& g, Vec3 q, CapState<K, M>& st) {
+    static_assert(M >= K + 8, "the buffer must hold the K best rows plus room to grow");
+    TopK<K> t;
+    t.init(st.lim);
+    cap_drain<K, M>(g, q, t, st.buf, st.cnt);
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        if (t.key[j] != kInfKey) { st.buf[n * kCapStride] = (uint32_t)(t.key[j] & 0xFFFFFFFFull); ++n; }
+    }
+    st.cnt = n;
+    if (n == K) st.lim = t.key[K - 1] + 1ull;
+}
+
+template <int K, int M>
+PCD_DEV void cap_scan(const GridView& g, Vec3 q, CapState<K, M>& st, uint32_t s, uint32_t e) {
+    // groups of 4 rows: 4 loads in flight per lane; the buffer keeps 4 rows of slack for the group's appends
+#pragma unroll 1
+    for (uint32_t r = s; r < e; r += 4) {
+        if (st.cnt > M - 4) cap_overflow<K, M>(g, q, st);
+        float4 p[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) p[u] = g.pts[min(r + u, e - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const unsigned long long c = cand_key<false>(q, p[u], r + u);
+            if (r + u < e && c < st.lim) {
+                st.buf[st.cnt * kCapStride] = r + u;
+                ++st.cnt;
+            }
+        }
+    }
+}
+
+template <int K, int M>
+PCD_DEV void cap_visit(const GridView& g, Vec3 q, int cx, int cy, int cz, CapState<K, M>& st) {
+    const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
+    const float gx = axis_gap(q.x, lx, lx + g.h), gy = axis_gap(q.y, ly, ly + g.h), gz = axis_gap(q.z, lz, lz + g.h);
+    if (gx * gx + gy * gy + gz * gz > st.kth() * 1.00001f + 1e-30f) return;
+    uint32_t s, e;
+    if (cell_range(g, cx, cy, cz, s, e)) cap_scan<K, M>(g, q, st, s, e);
+}
+
+template <int K, int M>
+PCD_DEV void knn_search_capped(const GridView& g, Vec3 q, TopK<K>& tk, unsigned long long cap, uint32_t* buf) {
+    CapState<K, M> st{cap, 0, buf};
+    const int cx = min(max(cell_coord(q.x, g.ox, g.inv_h), 0), g.dx - 1);
+    const int cy = min(max(cell_coord(q.y, g.oy, g.inv_h), 0), g.dy - 1);
+    const int cz = min(max(cell_coord(q.z, g.oz, g.inv_h), 0), g.dz - 1);
+#pragma unroll 1
+    for (int t = 0; t < 27; ++t) cap_visit<K, M>(g, q, cx + kRing1[t][0], cy + kRing1[t][1], cz + kRing1[t][2], st);
+    int R = 1;
+#pragma unroll 1
+    while (!search_done(g, q, cx, cy, cz, R, st.kth())) {
+        ++R;
+        if (R > 24) {  // pathological outlier: exhaustive scan from an empty buffer
+            st.cnt = 0;
+            st.lim = cap;
+            cap_scan<K, M>(g, q, st, 0, (uint32_t)g.n);
+            break;
+        }
+#pragma unroll 1
+        for (int dz = -R; dz <= R; ++dz) {
+#pragma unroll 1
+            for (int dy = -R; dy <= R; ++dy) {
+                const bool rim = (dz == -R || dz == R || dy == -R || dy == R);
+                const int step = rim ? 1 : 2 * R;
+#pragma unroll 1
+                for (int dx = -R; dx <= R; dx += step) cap_visit<K, M>(g, q, cx + dx, cy + dy, cz + dz, st);
+            }
+        }
+    }
+    tk.init(st.lim);
+    cap_drain<K, M>(g, q, tk, buf, st.cnt);
+#ifdef PCD_KNN_STATS
+    tk.stat[3] += st.cnt;  // rows left in the buffer at the end
+#endif
+}
+
 }  // namespace pcd

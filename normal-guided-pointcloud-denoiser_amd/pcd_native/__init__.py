@@ -17,6 +17,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PCD_LIB", os.path.join(os.path.dirname(_HERE), "libpcd.so"))
 
 PCD_OK, PCD_ERR_ARG, PCD_ERR_OOM, PCD_ERR_HIP, PCD_ERR_STATE, PCD_ERR_RCCL = 0, -1, -2, -3, -4, -5
+FIELD_POS, FIELD_NRM, FIELD_FN = 0, 1, 2
+(STAGE_KNN_NVT1, STAGE_NVT2, STAGE_PHASE_SUM, STAGE_PHASE_CENTRE, STAGE_PHASE_MAXDIST, STAGE_PHASE_APPLY,
+ STAGE_FINISH) = range(7)
 STEP_FLAT, STEP_EDGE, STEP_FEATURE, STEP_CORNER, STEP_NEW, STEP_DUMMY = range(6)
 
 
@@ -41,12 +44,13 @@ _SIGS = {
     "pcd_last_error": (ctypes.c_char_p, []),
     "pcd_version": (c_int, []),
     "pcd_max_k": (c_int, []),
-    "pcd_grid_build": (c_int, [c_void_p, c_int64, c_int, c_float, c_void_p, POINTER(c_void_p)]),
+    "pcd_grid_build": (c_int, [c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, POINTER(c_void_p)]),
+    "pcd_grid_params": (c_int, [c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, c_void_p]),
     "pcd_grid_destroy": (c_int, [c_void_p]),
     "pcd_grid_get_info": (c_int, [c_void_p, POINTER(_GridInfo)]),
     "pcd_grid_perm": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_knn": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
-    "pcd_knn_stats": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
+    "pcd_knn_stats": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p]),
     "pcd_nvt_csr": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p,
                             c_void_p, c_void_p]),
     "pcd_vu_smooth": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p, c_void_p]),
@@ -65,6 +69,12 @@ _SIGS = {
     "pcd_denoiser_set_timing": (c_int, [c_void_p, c_int]),
     "pcd_denoiser_reset_seed": (c_int, [c_void_p]),
     "pcd_denoiser_set_seeding": (c_int, [c_void_p, c_int]),
+    "pcd_denoiser_check": (c_int, [c_void_p, c_void_p]),
+    "pcd_denoiser_set_rows": (c_int, [c_void_p, c_void_p, c_int64]),
+    "pcd_denoiser_set_coverage": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "pcd_denoiser_stage": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "pcd_denoiser_pack": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
+    "pcd_denoiser_unpack": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "pcd_denoiser_get_timing": (c_int, [c_void_p, POINTER(c_float), c_int, POINTER(c_int)]),
     "pcd_orient_normals_mst": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64]),
     "pcd_host_eigh3": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
@@ -142,14 +152,18 @@ def i64(t):
 class Grid:
     """Frozen snapshot + kNN index (pcd_grid).  Mirrors the KDTree made in Selector.__init__."""
 
-    def __init__(self, xyz: torch.Tensor, k_hint: int = 16, cell: float = 0.0):
+    def __init__(self, xyz: torch.Tensor, k_hint: int = 16, cell: float = 0.0, origin=None):
+        """origin: optional (3,) lattice origin (needs cell > 0), see pcd_grid_build."""
         L = lib()
         x = f32(xyz)
         assert x.dim() == 2 and x.size(1) == 3
         self._keep = x
         h = c_void_p()
-        check(L.pcd_grid_build(ptr(x), x.size(0), int(k_hint), float(cell), c_void_p(stream_ptr()), ctypes.byref(h)),
-              "pcd_grid_build")
+        org = None
+        if origin is not None:
+            org = (ctypes.c_float * 3)(*[float(v) for v in origin])
+        check(L.pcd_grid_build(ptr(x), x.size(0), int(k_hint), float(cell), org, c_void_p(stream_ptr()),
+                               ctypes.byref(h)), "pcd_grid_build")
         self.handle = h
         self.n = x.size(0)
         self._keep = None
@@ -181,11 +195,12 @@ class Grid:
                             ptr(d2), c_void_p(stream_ptr())), "pcd_knn")
         return (idx, d2) if with_d2 else idx
 
-    def knn_stats(self, q: torch.Tensor, k: int) -> dict:
-        """Per-query averages of the kNN search work (diagnostic build of the search)."""
+    def knn_stats(self, q: torch.Tensor, k: int, batched: bool = False) -> dict:
+        """Per-query averages of the kNN search work (diagnostic build of the search; batched or insertion)."""
         q = f32(q)
         out = torch.zeros(6, dtype=torch.int64, device=q.device)
-        check(lib().pcd_knn_stats(self.handle, ptr(q), q.size(0), int(k), ptr(out), c_void_p(stream_ptr())),
+        check(lib().pcd_knn_stats(self.handle, ptr(q), q.size(0), int(k), int(bool(batched)), ptr(out),
+                                  c_void_p(stream_ptr())),
               "pcd_knn_stats")
         v = out.cpu().double() / max(q.size(0), 1)
         names = ["cells_considered", "cells_probed", "cells_found", "candidates", "inserts", "extra_rings"]
@@ -236,6 +251,42 @@ class FusedDenoiser:
 
     def set_timing(self, on: bool):
         check(lib().pcd_denoiser_set_timing(self.handle, int(on)), "pcd_denoiser_set_timing")
+
+    def check(self):
+        check(lib().pcd_denoiser_check(self.handle, c_void_p(stream_ptr())), "pcd_denoiser_check")
+
+    # ---- spatial slabs: active rows, coverage, staged iteration, halo pack/unpack (include/pcd.h)
+    def set_rows(self, rows):
+        """rows: int32 device tensor of spatial-order rows (kept alive here), or None for all rows."""
+        self._rows = None if rows is None else rows.contiguous()
+        n = 0 if rows is None else self._rows.numel()
+        check(lib().pcd_denoiser_set_rows(self.handle, ptr(self._rows), n), "pcd_denoiser_set_rows")
+
+    def set_coverage(self, lo=None, hi=None):
+        if lo is None:
+            check(lib().pcd_denoiser_set_coverage(self.handle, None, None), "pcd_denoiser_set_coverage")
+            return
+        lo3 = (c_float * 3)(*[float(v) for v in lo])
+        hi3 = (c_float * 3)(*[float(v) for v in hi])
+        check(lib().pcd_denoiser_set_coverage(self.handle, lo3, hi3), "pcd_denoiser_set_coverage")
+
+    def stage(self, params: DenoiseParams, stage: int, phase: int = 0, red: torch.Tensor = None):
+        check(lib().pcd_denoiser_stage(self.handle, ctypes.byref(params), int(stage), int(phase), ptr(red),
+                                       c_void_p(stream_ptr())), "pcd_denoiser_stage")
+
+    def pack(self, field: int, rows: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+        n = rows.numel()
+        if out is None:
+            out = torch.empty((n, 4), dtype=torch.float32, device=rows.device)
+        check(lib().pcd_denoiser_pack(self.handle, int(field), ptr(rows), n, ptr(out), c_void_p(stream_ptr())),
+              "pcd_denoiser_pack")
+        return out
+
+    def unpack(self, field: int, rows: torch.Tensor, data: torch.Tensor):
+        data = data.contiguous()
+        assert data.dtype == torch.float32 and data.shape == (rows.numel(), 4)
+        check(lib().pcd_denoiser_unpack(self.handle, int(field), ptr(rows), rows.numel(), ptr(data),
+                                        c_void_p(stream_ptr())), "pcd_denoiser_unpack")
 
     def timing(self):
         buf = (c_float * 8)()
@@ -310,6 +361,16 @@ def edge_length_sum(pos, a, b):
 def mesh_update(v, f, fn, vf, ni, k):
     check(lib().pcd_mesh_update(ptr(v), v.size(0), ptr(f), ptr(fn), f.size(0), ptr(vf), ptr(ni), int(k),
                                 c_void_p(stream_ptr())), "pcd_mesh_update")
+
+
+def grid_params(xyz: torch.Tensor, k_hint: int = 16, cell: float = 0.0):
+    """(origin (3,), cell edge) of the lattice pcd_grid_build would use for xyz."""
+    x = f32(xyz)
+    org = (ctypes.c_float * 3)()
+    h = ctypes.c_float()
+    check(lib().pcd_grid_params(ptr(x), x.size(0), int(k_hint), float(cell), org, ctypes.byref(h),
+                                c_void_p(stream_ptr())), "pcd_grid_params")
+    return [org[0], org[1], org[2]], h.value
 
 
 def host_eigh3(t6):

@@ -1,0 +1,323 @@
+"""Spatial-slab multi-GPU denoising: one process per GPU, RCCL halo exchange.
+
+The frozen snapshot is cut into P slabs of equal point count along its longest bbox axis.  Rank r owns the points
+of slab r and holds, in addition, a HALO: every snapshot point whose coordinate on that axis lies within `halo`
+of the slab.  Its grid is built over owned + halo points on the global cell lattice (pcd_grid_params), so its
+spatial order is a subsequence of the one-GPU order and distance ties break exactly as on one GPU.
+
+Per iteration the rank runs the fused loop's stages on its OWN rows only (pcd_denoiser_stage) and keeps the halo
+rows current between stages (the only places a stage reads another rank's points):
+    KNN_NVT1                        kNN + first vote + VU smoothing of own points
+    exchange FN                     NVT2 reads the smoothed normals of the neighbours
+    NVT2                            classes + edge vectors
+    per phase: [flat/new: SUM -> all-reduce(sum) -> CENTRE -> MAXDIST -> all-reduce(max)] APPLY -> exchange POS
+    FINISH                          n := f_n (the halo rows' f_n arrived with the FN exchange)
+The global flat centre / delta (Denoiser.py:106-107) are the only collectives; halo traffic is point-to-point
+between slab neighbours.  Exactness is checked, not assumed: every k-ball must stay inside the slab widened by the
+halo (pcd_denoiser_set_coverage), otherwise check() raises (halo too thin).
+
+The driver is engine-agnostic: `HipSlabEngine` (libpcd, the product path) or any object with the same methods
+(the CPU tests use an oracle engine, tests/slab_cpu_engine.py).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+import pcd_native as nat
+
+
+# ----------------------------------------------------------------------------------------------- partition
+@dataclass
+class SlabPlan:
+    """Owned / halo membership of every rank, identical on all ranks (computed from the same snapshot)."""
+    world: int
+    axis: int
+    halo: float
+    owner: torch.Tensor                         # int64 [N]: rank owning each snapshot point
+    lo: list                                    # per rank: min coordinate of the owned points on `axis`
+    hi: list                                    # per rank: max coordinate
+    local: list = field(default_factory=list)   # per rank: int64 global indices of owned + halo, ascending
+
+    @staticmethod
+    def build(snap: torch.Tensor, world: int, halo: float, axis: int | None = None) -> "SlabPlan":
+        snap = snap.detach()
+        n = snap.size(0)
+        assert world >= 1 and n >= world, "need at least one point per rank"
+        ext = snap.max(0).values - snap.min(0).values
+        if axis is None:
+            axis = int(torch.argmax(ext).item())
+        key = snap[:, axis].contiguous()
+        order = torch.sort(key, stable=True).indices           # ties by index: deterministic on every rank
+        owner = torch.empty(n, dtype=torch.int64, device=snap.device)
+        bounds = [(r * n) // world for r in range(world + 1)]
+        lo, hi, local = [], [], []
+        for r in range(world):
+            owner[order[bounds[r]:bounds[r + 1]]] = r
+        for r in range(world):
+            ks = key[order[bounds[r]:bounds[r + 1]]]
+            lo.append(float(ks[0]))
+            hi.append(float(ks[-1]))
+        for r in range(world):
+            inside = (key >= lo[r] - halo) & (key <= hi[r] + halo)
+            local.append(torch.nonzero(inside | (owner == r)).flatten())
+        return SlabPlan(world, axis, float(halo), owner, lo, hi, local)
+
+    def coverage(self, r: int):
+        """Box the rank's local snapshot covers: the slab widened by the halo on `axis` (open ends at the outer
+        slabs and on the other axes)."""
+        big = 3.0e38
+        lo, hi = [-big] * 3, [big] * 3
+        if r > 0:
+            lo[self.axis] = self.lo[r] - self.halo
+        if r < self.world - 1:
+            hi[self.axis] = self.hi[r] + self.halo
+        return lo, hi
+
+    def transfer(self, src: int, dst: int) -> torch.Tensor:
+        """Global indices (ascending) of points owned by `src` that `dst` holds as halo."""
+        loc = self.local[dst]
+        return loc[self.owner[loc] == src]
+
+
+# ----------------------------------------------------------------------------------------------- transport
+class TorchTransport:
+    """Halo exchange and scalar all-reduces over torch.distributed: NCCL (= RCCL on ROCm, over xGMI) moves device
+    tensors directly; gloo stages through host memory."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.host = dist.get_backend(group) == "gloo"
+
+    def exchange(self, sends: dict, recv_shapes: dict, device) -> dict:
+        """sends: peer -> tensor; recv_shapes: peer -> shape.  Returns peer -> received tensor on `device`."""
+        dist = self.dist
+        ops, outs, staged = [], {}, {}
+        for peer, shape in recv_shapes.items():
+            buf = torch.empty(shape, dtype=torch.float32, device="cpu" if self.host else device)
+            outs[peer] = buf
+            ops.append(dist.P2POp(dist.irecv, buf, peer, self.group))
+        for peer, t in sends.items():
+            staged[peer] = t.cpu() if self.host else t.contiguous()
+            ops.append(dist.P2POp(dist.isend, staged[peer], peer, self.group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return {p: (b.to(device) if self.host else b) for p, b in outs.items()}
+
+    def all_reduce(self, t: torch.Tensor, op: str) -> torch.Tensor:
+        dist = self.dist
+        red = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX}[op]
+        if self.host and t.device.type != "cpu":
+            h = t.cpu()
+            dist.all_reduce(h, red, self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, red, self.group)
+        return t
+
+
+class LocalTransport:
+    """world = 1: nothing to exchange."""
+    rank, world = 0, 1
+
+    def exchange(self, sends, recv_shapes, device):
+        assert not sends and not recv_shapes
+        return {}
+
+    def all_reduce(self, t, op):
+        return t
+
+
+# ----------------------------------------------------------------------------------------------- HIP engine
+class HipSlabEngine:
+    """libpcd's fused loop over one rank's local snapshot (owned + halo), driven stage by stage."""
+
+    def __init__(self, local_pos, local_n, owned_local, k_max, origin, cell, coverage, seeding=True):
+        dev = nat.device()
+        self.device = dev
+        self.grid = nat.Grid(local_pos.to(dev), cell=cell, origin=origin)
+        perm = self.grid.perm().long()                      # spatial row -> local index
+        self.row_of = torch.empty_like(perm)
+        self.row_of[perm] = torch.arange(perm.numel(), device=dev)
+        self.n = perm.numel()
+        self.fused = nat.FusedDenoiser(self.grid, k_max)
+        self.fused.load(local_pos.to(dev), local_n.to(dev))
+        self.fused.set_seeding(seeding)
+        own_rows = torch.sort(self.row_of[owned_local.to(dev)]).values.to(torch.int32)
+        self.fused.set_rows(own_rows)
+        self.fused.set_coverage(*coverage)
+        self.red4 = torch.zeros(4, dtype=torch.float64, device=dev)
+        self.red1 = torch.zeros(1, dtype=torch.float32, device=dev)
+
+    def rows(self, local_idx: torch.Tensor) -> torch.Tensor:
+        return self.row_of[local_idx.to(self.device)].to(torch.int32).contiguous()
+
+    def stage(self, params, stage, phase=0, red=None):
+        self.fused.stage(params, stage, phase, red)
+
+    def pack(self, fld, rows):
+        return self.fused.pack(fld, rows)
+
+    def unpack(self, fld, rows, data):
+        self.fused.unpack(fld, rows, data)
+
+    def check(self):
+        self.fused.check()
+
+    def store(self):
+        pos = torch.empty((self.n, 3), dtype=torch.float32, device=self.device)
+        n = torch.empty_like(pos)
+        self.fused.store(pos, n)
+        return pos, n
+
+
+# ----------------------------------------------------------------------------------------------- driver
+class SlabDenoiser:
+    """The body of Processor.denoise (Processor.py:119-139) over spatial slabs, one rank per GPU.
+
+    snap_pos / snap_n: the WHOLE cloud (identical on every rank; the frozen snapshot is the initial positions,
+    as in Selector.__init__).  halo: slab widening in snapshot units (None: 3x the largest k-th neighbour distance
+    of a sample, see default_halo)."""
+
+    def __init__(self, snap_pos, snap_n, k_max, transport=None, halo=None, engine_factory=None, seeding=True,
+                 k_hint=32):
+        self.t = transport or LocalTransport()
+        rank, world = self.t.rank, self.t.world
+        if halo is None:
+            halo = default_halo(snap_pos, k_max)
+        self.plan = SlabPlan.build(snap_pos, world, halo)
+        plan = self.plan
+        self.local = plan.local[rank]                           # global ids, ascending
+        pos_l, n_l = snap_pos[self.local], snap_n[self.local]
+        owned_mask = plan.owner[self.local] == rank
+        self.owned_local = torch.nonzero(owned_mask).flatten()
+        self.owned_global = self.local[self.owned_local]
+        if engine_factory is None:
+            origin, cell = nat.grid_params(snap_pos.to(nat.device()), k_hint=k_hint)
+            self.e = HipSlabEngine(pos_l, n_l, self.owned_local, k_max, origin, cell, plan.coverage(rank), seeding)
+        else:
+            self.e = engine_factory(pos_l, n_l, self.owned_local, k_max, plan.coverage(rank))
+        # halo routes: rows I send to each peer and rows I receive from it (both ascending global index)
+        to_local = torch.full((snap_pos.size(0),), -1, dtype=torch.int64, device=self.local.device)
+        to_local[self.local] = torch.arange(self.local.numel(), device=self.local.device)
+        self.send_rows, self.recv_rows = {}, {}
+        for peer in range(world):
+            if peer == rank:
+                continue
+            out = plan.transfer(rank, peer)
+            inc = plan.transfer(peer, rank)
+            if out.numel():
+                self.send_rows[peer] = self.e.rows(to_local[out])
+            if inc.numel():
+                self.recv_rows[peer] = self.e.rows(to_local[inc])
+        self.halo_points = sum(r.numel() for r in self.recv_rows.values())
+
+    def _exchange(self, fld):
+        sends = {p: self.e.pack(fld, rows) for p, rows in self.send_rows.items()}
+        shapes = {p: (rows.numel(), 4) for p, rows in self.recv_rows.items()}
+        dev = next(iter(self.recv_rows.values())).device if self.recv_rows else None
+        got = self.t.exchange(sends, shapes, dev)
+        for p, data in got.items():
+            self.e.unpack(fld, self.recv_rows[p], data)
+
+    def _phases(self, params):
+        e, t = self.e, self.t
+        for ph in range(params.nphases):
+            if params.phase_kind[ph] in (nat.STEP_FLAT, nat.STEP_NEW):
+                red4 = e.red4
+                e.stage(params, nat.STAGE_PHASE_SUM, ph, red4)
+                t.all_reduce(red4, "sum")
+                e.stage(params, nat.STAGE_PHASE_CENTRE, ph, red4)
+                red1 = e.red1
+                e.stage(params, nat.STAGE_PHASE_MAXDIST, ph, red1)
+                t.all_reduce(red1, "max")
+                e.stage(params, nat.STAGE_PHASE_APPLY, ph, red1)
+            else:
+                e.stage(params, nat.STAGE_PHASE_APPLY, ph, None)
+            self._exchange(nat.FIELD_POS)
+
+    def iterate(self, params, iterations: int = 1):
+        e = self.e
+        for _ in range(iterations):
+            e.stage(params, nat.STAGE_KNN_NVT1)
+            self._exchange(nat.FIELD_FN)
+            e.stage(params, nat.STAGE_NVT2)
+            self._phases(params)
+            e.stage(params, nat.STAGE_FINISH)
+
+    def iterate_timed(self, params) -> dict:
+        """One iteration with CUDA/HIP events on the launch stream around each stage group (ms)."""
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        e = self.e
+        ev[0].record()
+        e.stage(params, nat.STAGE_KNN_NVT1)
+        ev[1].record()
+        self._exchange(nat.FIELD_FN)
+        ev[2].record()
+        e.stage(params, nat.STAGE_NVT2)
+        ev[3].record()
+        self._phases(params)
+        ev[4].record()
+        e.stage(params, nat.STAGE_FINISH)
+        ev[5].record()
+        ev[5].synchronize()
+        names = ["knn_nvt1", "fn_exchange", "nvt2", "phases_with_exchange", "finish"]
+        return {nm: ev[i].elapsed_time(ev[i + 1]) for i, nm in enumerate(names)}
+
+    def check(self):
+        self.e.check()
+
+    def owned_state(self):
+        """(global ids, positions, normals) of this rank's own points."""
+        pos, n = self.e.store()
+        idx = self.owned_local.to(pos.device)
+        return self.owned_global, pos[idx], n[idx]
+
+
+def default_halo(snap_pos: torch.Tensor, k: int, sample: int = 65536, factor: float = 3.0) -> float:
+    """factor x the largest k-th neighbour distance over an even sample of snapshot points (queries are current
+    positions, which drift from the snapshot; the coverage check reports a halo that turns out too thin)."""
+    dev = nat.device()
+    pos = snap_pos.to(dev)
+    g = nat.Grid(pos, k_hint=k)
+    stride = max(1, pos.size(0) // sample)
+    q = pos[::stride].contiguous()
+    _, d2 = g.knn(q, k, with_d2=True)
+    return factor * math.sqrt(float(d2[:, -1].max()))
+
+
+def gather_global(state, n_total: int, transport) -> tuple:
+    """All-gather every rank's (ids, pos, n) into global arrays (tests / final output)."""
+    ids, pos, n = state
+    if transport.world == 1:
+        out_p = torch.empty((n_total, 3), dtype=pos.dtype, device=pos.device)
+        out_n = torch.empty_like(out_p)
+        out_p[ids.to(pos.device)] = pos
+        out_n[ids.to(pos.device)] = n
+        return out_p, out_n
+    dist = transport.dist
+    pay = torch.cat([ids.to(torch.float64)[:, None], pos.double(), n.double()], 1)
+    dev = "cpu" if transport.host else pay.device
+    pay = pay.to(dev)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(transport.world)]
+    dist.all_gather(sizes, torch.tensor([pay.size(0)], dtype=torch.int64, device=dev), transport.group)
+    mx = int(max(s.item() for s in sizes))
+    padded = torch.zeros((mx, 7), dtype=torch.float64, device=dev)
+    padded[: pay.size(0)] = pay
+    bufs = [torch.zeros_like(padded) for _ in range(transport.world)]
+    dist.all_gather(bufs, padded, transport.group)
+    out_p = torch.empty((n_total, 3), dtype=torch.float32)
+    out_n = torch.empty_like(out_p)
+    for b, s in zip(bufs, sizes):
+        b = b[: int(s.item())].cpu()
+        gi = b[:, 0].long()
+        out_p[gi] = b[:, 1:4].float()
+        out_n[gi] = b[:, 4:7].float()
+    return out_p, out_n

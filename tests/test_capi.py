@@ -52,7 +52,7 @@ def test_argument_errors_are_reported():
     rc = L.pcd_knn(None, None, 10, 8, None, 64, 0, 0, None, None)
     assert rc == nat.PCD_ERR_ARG
     assert b"grid is null" in L.pcd_last_error()
-    rc = L.pcd_grid_build(None, 0, 16, 0.0, None, ctypes.byref(idx))
+    rc = L.pcd_grid_build(None, 0, 16, 0.0, None, None, ctypes.byref(idx))
     assert rc == nat.PCD_ERR_ARG and not idx.value
     with pytest.raises(ValueError):
         nat.check(L.pcd_step_csr(99, None, None, None, 0, None, None, None, 0, 1.0, 1.0, None, None), "step")

@@ -1,0 +1,99 @@
+"""Spatial slabs on the GPU: the staged HIP engine against the one-GPU fused loop, with one rank
+and with two ranks sharing the box's GPU over gloo (RCCL needs one GPU per rank; the 8-GPU RCCL run is the
+driver's bench)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+import pcd_native as nat
+from pcd_slab import LocalTransport, SlabDenoiser, TorchTransport, gather_global, default_halo
+
+K, KU, ITERS = 32, 8, 3
+
+
+def _cloud(dev, n=60000, seed=11):
+    from bench import make_cloud
+    pos, nrm, _ = make_cloud(n, seed, dev)
+    return pos, nrm
+
+
+def _d(pos):
+    from Pointcloud.Modules.Object import Pointcloud
+    from Pointcloud.Modules.Processor import Processor
+    return 2 * float(Processor(Pointcloud(pos.clone())).meanEdgeLength())
+
+
+def _fused(pos, nrm, d):
+    g = nat.Grid(pos, k_hint=K)
+    fd = nat.FusedDenoiser(g, max(K, KU))
+    fd.load(pos, nrm)
+    fd.iterate(nat.make_params(k=K, k_update=KU, d=d), ITERS)
+    p, n = torch.empty_like(pos), torch.empty_like(nrm)
+    fd.store(p, n)
+    return p.cpu().numpy(), n.cpu().numpy()
+
+
+@pytest.mark.gpu
+def test_hip_slab_world1_is_the_fused_loop(gpu):
+    pos, nrm = _cloud(gpu)
+    d = _d(pos)
+    sd = SlabDenoiser(pos, nrm, max(K, KU), transport=LocalTransport(), k_hint=K)
+    sd.iterate(nat.make_params(k=K, k_update=KU, d=d), ITERS)
+    sd.check()
+    p, n = gather_global(sd.owned_state(), pos.size(0), sd.t)
+    rp, rn = _fused(pos, nrm, d)
+    np.testing.assert_array_equal(p.cpu().numpy(), rp)
+    np.testing.assert_array_equal(n.cpu().numpy(), rn)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_path, d):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        pos, nrm = _cloud(dev)
+        tr = TorchTransport()
+        sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K)
+        sd.iterate(nat.make_params(k=K, k_update=KU, d=d), ITERS)
+        sd.check()
+        p, n = gather_global(sd.owned_state(), pos.size(0), tr)
+        if rank == 0:
+            np.savez(out_path, pos=p.numpy(), n=n.numpy(), halo=sd.halo_points)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_hip_slab_world2_matches_one_gpu(gpu, tmp_path):
+    import torch.multiprocessing as mp
+    pos, nrm = _cloud(gpu)
+    d = _d(pos)
+    out = str(tmp_path / "slab2.npz")
+    mp.spawn(_worker, args=(2, _free_port(), out, d), nprocs=2, join=True)
+    res = np.load(out)
+    assert int(res["halo"]) > 0
+    rp, rn = _fused(pos, nrm, d)
+    bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
+    # same kernels and tie-breaks; only the f64 summation order of the global flat centre differs
+    np.testing.assert_allclose(res["pos"], rp, rtol=0, atol=1e-6 * bbox)
+    np.testing.assert_allclose(res["n"], rn, rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_default_halo_covers_knn(gpu):
+    pos, _ = _cloud(gpu, 20000)
+    h = default_halo(pos, K)
+    _, d2 = nat.Grid(pos, k_hint=K).knn(pos, K, with_d2=True)
+    assert h >= 2.9 * float(d2[:, -1].max().sqrt())
