@@ -101,7 +101,8 @@ def main():
     ap.add_argument("--k-update", type=int, default=8)
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--seeding", action="store_true", help="cap each kNN search at last iteration's list")
+    ap.add_argument("--no-seeding", dest="seeding", action="store_false",
+                    help="run every kNN search unseeded (the seeded search is the default; identical results)")
     ap.add_argument("--profile-steps", type=int, default=5, help="extra per-kernel timed iterations (HIP events)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: independent clouds per rank instead of spatial slabs of one global cloud")
@@ -128,7 +129,11 @@ def main():
         # one global cloud of world x P points (identical on every rank), cut into spatial slabs with a halo
         from pcd_slab import SlabDenoiser, TorchTransport
         pos, nrm, diag = make_cloud(args.points * world, 3, dev)
-        d = 2 * float(Processor(Pointcloud(pos), k_hint=args.k).meanEdgeLength())
+        dist.broadcast(pos, 0)       # one cloud: rank 0's (device sampling is not bit-reproducible across ranks)
+        dist.broadcast(nrm, 0)
+        dt = torch.tensor([2 * float(Processor(Pointcloud(pos), k_hint=args.k).meanEdgeLength())], device=dev)
+        dist.broadcast(dt, 0)
+        d = float(dt)
         sd = SlabDenoiser(pos, nrm, max(args.k, args.k_update), transport=TorchTransport(), k_hint=args.k,
                           seeding=args.seeding)
         del pos, nrm

@@ -149,8 +149,9 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
  * are those of the LAST iteration's NVT2; f_n is the last smoothed normal field (= n after iterate). */
 int pcd_denoiser_store(pcd_denoiser* dn, float* pos, float* n, int64_t* classes, float* edge_vectors,
                        void* stream);
-/* Seeded search (default off): iterations after the first cap the acceptance threshold at the largest key of
- * the previous iteration's stored list.  Results are identical either way; it only changes the work done.
+/* Seeded search (default ON): iterations after the first cap the acceptance threshold at the largest key of
+ * the previous iteration's stored list (re-keyed at the current positions) and run the capped search (LDS row
+ * buffer, one sorted drain).  Results are identical either way (tested bitwise); it only changes the work done.
  * reset_seed forgets the stored list, so the next iterate() runs unseeded. */
 int pcd_denoiser_set_seeding(pcd_denoiser* dn, int enable);
 int pcd_denoiser_reset_seed(pcd_denoiser* dn);

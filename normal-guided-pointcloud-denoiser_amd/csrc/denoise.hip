@@ -30,6 +30,13 @@ struct ColNb {
     int64_t n, i;
     PCD_DEV int64_t operator()(int t) const { return idx[(int64_t)t * n + i]; }
 };
+// Same, for a list read exactly once (NVT2): streamed past L2 so the neighbour gathers keep it.
+struct ColNbStream {
+    const int32_t* idx;
+    int64_t n, i;
+    PCD_DEV int64_t operator()(int t) const { return __builtin_nontemporal_load(idx + (int64_t)t * n + i); }
+};
+typedef float v4f __attribute__((ext_vector_type(4)));
 struct RegNb32 {
     const int* l;
     PCD_DEV int64_t operator()(int t) const { return l[t]; }
@@ -99,7 +106,7 @@ __global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __re
         // all list rows first (K loads in flight), then their points; columns >= kstore re-read column 0
         uint32_t sd[K];
 #pragma unroll
-        for (int t = 0; t < K; ++t) sd[t] = (uint32_t)idx[(int64_t)(t < kstore ? t : 0) * N + i];
+        for (int t = 0; t < K; ++t) sd[t] = (uint32_t)__builtin_nontemporal_load(idx + (int64_t)(t < kstore ? t : 0) * N + i);
         cap = 0ull;
 #pragma unroll
         for (int t = 0; t < K; ++t) {
@@ -126,7 +133,7 @@ __global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __re
         if (t < kstore) {
             // a list entry that is not a point would be an internal error: record it, never fault on it
             if ((uint32_t)l[t] >= (uint32_t)N) { bad = true; l[t] = (int)i; }
-            idx[(int64_t)t * N + i] = l[t];
+            __builtin_nontemporal_store(l[t], idx + (int64_t)t * N + i);   // streamed: keep L2 for the gathers
         }
     }
     if (bad) atomicOr(err, 1);
@@ -135,7 +142,8 @@ __global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __re
     float w[3], V[3][3];
     eigh3(T, w, V);
     const float4 n4 = nrm[i];
-    store4(fn, i, vu_smooth(w, V, v3(n4.x, n4.y, n4.z), tau, damp));
+    const Vec3 f = vu_smooth(w, V, v3(n4.x, n4.y, n4.z), tau, damp);
+    __builtin_nontemporal_store(v4f{f.x, f.y, f.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
 }
 
 // K2: NVT2 on f_n -> classes + edge vectors.
@@ -148,7 +156,7 @@ __global__ __launch_bounds__(256) void k_nvt2(const float4* __restrict__ pos, co
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 p4 = pos[i];
-    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{fn}, v3(p4.x, p4.y, p4.z), k, ColNb{idx, N, i}, rho);
+    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{fn}, v3(p4.x, p4.y, p4.z), k, ColNbStream{idx, N, i}, rho);
     float w[3], V[3][3];
     eigh3(T, w, V);
     cls[i] = (uint8_t)classify(w, scale, nullptr);
@@ -283,7 +291,7 @@ struct pcd_denoiser {
     int64_t n_rows = 0;
     Cover cov{{1.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};  // disabled
     int seed_cols = 0;            // columns of idx holding a valid kNN list of the snapshot (0: none yet)
-    bool seeding = false;         // use the stored list as an acceptance cap (pcd_denoiser_set_seeding)
+    bool seeding = true;          // use the stored list as an acceptance cap (pcd_denoiser_set_seeding)
     bool loaded = false, iterated = false;
     bool timing = false;
     std::vector<hipEvent_t> ev;

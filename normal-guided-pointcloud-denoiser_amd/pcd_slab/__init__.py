@@ -111,6 +111,15 @@ class TorchTransport:
                 req.wait()
         return {p: (b.to(device) if self.host else b) for p, b in outs.items()}
 
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.host and t.device.type != "cpu":
+            h = t.cpu()
+            self.dist.broadcast(h, src, self.group)
+            t.copy_(h)
+        else:
+            self.dist.broadcast(t, src, self.group)
+        return t
+
     def all_reduce(self, t: torch.Tensor, op: str) -> torch.Tensor:
         dist = self.dist
         red = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX}[op]
@@ -132,6 +141,9 @@ class LocalTransport:
         return {}
 
     def all_reduce(self, t, op):
+        return t
+
+    def broadcast_(self, t, src=0):
         return t
 
 
@@ -182,14 +194,17 @@ class HipSlabEngine:
 class SlabDenoiser:
     """The body of Processor.denoise (Processor.py:119-139) over spatial slabs, one rank per GPU.
 
-    snap_pos / snap_n: the WHOLE cloud (identical on every rank; the frozen snapshot is the initial positions,
-    as in Selector.__init__).  halo: slab widening in snapshot units (None: 3x the largest k-th neighbour distance
+    snap_pos / snap_n: the WHOLE cloud (the frozen snapshot is the initial positions, as in Selector.__init__);
+    rank 0's copy is broadcast, so every rank plans from identical data.  halo: slab widening in snapshot units (None: 3x the largest k-th neighbour distance
     of a sample, see default_halo)."""
 
     def __init__(self, snap_pos, snap_n, k_max, transport=None, halo=None, engine_factory=None, seeding=True,
                  k_hint=32):
         self.t = transport or LocalTransport()
         rank, world = self.t.rank, self.t.world
+        if world > 1:
+            snap_pos = self.t.broadcast_(snap_pos.contiguous().clone())
+            snap_n = self.t.broadcast_(snap_n.contiguous().clone())
         if halo is None:
             halo = default_halo(snap_pos, k_max)
         self.plan = SlabPlan.build(snap_pos, world, halo)

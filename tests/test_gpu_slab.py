@@ -55,7 +55,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_path, d):
+def _worker(rank, world, port, out_path, cloud_path, d):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -63,7 +63,8 @@ def _worker(rank, world, port, out_path, d):
     try:
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        pos, nrm = _cloud(dev)
+        c = np.load(cloud_path)
+        pos, nrm = torch.from_numpy(c["pos"]).to(dev), torch.from_numpy(c["n"]).to(dev)
         tr = TorchTransport()
         sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K)
         sd.iterate(nat.make_params(k=K, k_update=KU, d=d), ITERS)
@@ -80,8 +81,9 @@ def test_hip_slab_world2_matches_one_gpu(gpu, tmp_path):
     import torch.multiprocessing as mp
     pos, nrm = _cloud(gpu)
     d = _d(pos)
-    out = str(tmp_path / "slab2.npz")
-    mp.spawn(_worker, args=(2, _free_port(), out, d), nprocs=2, join=True)
+    out, cloud = str(tmp_path / "slab2.npz"), str(tmp_path / "cloud.npz")
+    np.savez(cloud, pos=pos.cpu().numpy(), n=nrm.cpu().numpy())
+    mp.spawn(_worker, args=(2, _free_port(), out, cloud, d), nprocs=2, join=True)
     res = np.load(out)
     assert int(res["halo"]) > 0
     rp, rn = _fused(pos, nrm, d)
