@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-seeding", dest="seeding", action="store_false",
                     help="run every kNN search unseeded (the seeded search is the default; identical results)")
+    ap.add_argument("--no-anchoring", dest="anchoring", action="store_false",
+                    help="seeded searches without anchors (capped grid search every iteration; identical results)")
     ap.add_argument("--profile-steps", type=int, default=5, help="extra per-kernel timed iterations (HIP events)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: independent clouds per rank instead of spatial slabs of one global cloud")
@@ -147,6 +149,7 @@ def main():
         fused = proc._fused_for(max(args.k, args.k_update))
         fused.load(proc.graph.pos, proc.graph.n)
         fused.set_seeding(args.seeding)
+        fused.set_anchoring(args.anchoring)
         params = nat.make_params(k=args.k, k_update=args.k_update, d=d)
         step = lambda: fused.iterate(params, 1)  # noqa: E731
 

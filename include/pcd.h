@@ -155,6 +155,12 @@ int pcd_denoiser_store(pcd_denoiser* dn, float* pos, float* n, int64_t* classes,
  * reset_seed forgets the stored list, so the next iterate() runs unseeded. */
 int pcd_denoiser_set_seeding(pcd_denoiser* dn, int enable);
 int pcd_denoiser_reset_seed(pcd_denoiser* dn);
+/* Anchored search (default ON, applies to seeded searches with k, k_update <= 32): each point keeps an anchor --
+ * a position, the exact 2K nearest snapshot points there (K = the list cap 8/16/32) and their 2K-th distance D.
+ * When the current k-th distance over that list is below D - |q - anchor|, the list's top k IS the snapshot's
+ * k-NN (no grid search); the few queries that fail are re-anchored by a full grid search.  Same results (tested
+ * bitwise).  Anchors depend only on the snapshot: they survive load(); reset_seed drops them. */
+int pcd_denoiser_set_anchoring(pcd_denoiser* dn, int enable);
 /* Profiling aid: elapsed ms of each kernel class in the last iterate() when timing was enabled. */
 int pcd_denoiser_set_timing(pcd_denoiser* dn, int enable);
 int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n_written);

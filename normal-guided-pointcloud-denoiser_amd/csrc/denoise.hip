@@ -21,6 +21,7 @@
 
 #include "pcd_knn.h"
 #include "pcd_ops.h"
+#include "pcd_wknn.h"
 
 namespace pcd {
 int knn_cap(int k);
@@ -83,6 +84,40 @@ struct Cover {
     }
 };
 
+// K1 epilogue (every kNN variant): store the list column-major, check it, NVT1 + eigh + VU smoothing -> f_n.
+// dk = d² of the kstore-th neighbour.
+template <int K>
+PCD_DEV void k1_epilogue(const float4* __restrict__ pos, const float4* __restrict__ nrm, int64_t N, int64_t i,
+                         Vec3 vi, int (&l)[K], float dk, int k, int kstore, float rho, float tau, float damp,
+                         const Cover& cov, int32_t* __restrict__ idx, float4* __restrict__ fn, int* __restrict__ err) {
+    bool bad = false;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+        if (t < kstore) {
+            // a list entry that is not a point would be an internal error: record it, never fault on it
+            if ((uint32_t)l[t] >= (uint32_t)N) { bad = true; l[t] = (int)i; }
+            __builtin_nontemporal_store(l[t], idx + (int64_t)t * N + i);   // streamed: keep L2 for the gathers
+        }
+    }
+    if (bad) atomicOr(err, 1);
+    if (!cov.holds(vi, dk)) atomicOr(err, 2);
+#ifdef PCD_EXP_NONVT
+    const float4 n4 = nrm[i];
+    __builtin_nontemporal_store(v4f{n4.x, n4.y, n4.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
+#else
+    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho);
+    const float4 n4 = nrm[i];
+#ifdef PCD_EXP_NOEIGH
+    const Vec3 f = v3(T.a00 + n4.x, T.a01 + T.a11, T.a02 + T.a22 + T.a12);
+#else
+    float w[3], V[3][3];
+    eigh3(T, w, V);
+    const Vec3 f = vu_smooth(w, V, v3(n4.x, n4.y, n4.z), tau, damp);
+#endif
+    __builtin_nontemporal_store(v4f{f.x, f.y, f.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
+#endif
+}
+
 // K1: kNN + NVT1 + VU smoothing.
 // SEED (iterations after the first): the largest key of last iteration's list (kstore distinct snapshot points),
 // re-keyed at the current position, caps the acceptance threshold from the first candidate on, and the capped
@@ -124,26 +159,151 @@ __global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __re
         knn_search<K, false>(g, vi, tk);
     }
     int l[K];
-    bool bad = false;
     float dk = 0.f;                  // d² of the kstore-th neighbour (static select: no dynamic register index)
 #pragma unroll
     for (int t = 0; t < K; ++t) {
         l[t] = tk.idx(t);
         if (t == kstore - 1) dk = tk.d2(t);
-        if (t < kstore) {
-            // a list entry that is not a point would be an internal error: record it, never fault on it
-            if ((uint32_t)l[t] >= (uint32_t)N) { bad = true; l[t] = (int)i; }
-            __builtin_nontemporal_store(l[t], idx + (int64_t)t * N + i);   // streamed: keep L2 for the gathers
-        }
     }
-    if (bad) atomicOr(err, 1);
-    if (!cov.holds(vi, dk)) atomicOr(err, 2);
-    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho);
-    float w[3], V[3][3];
-    eigh3(T, w, V);
-    const float4 n4 = nrm[i];
-    const Vec3 f = vu_smooth(w, V, v3(n4.x, n4.y, n4.z), tau, damp);
-    __builtin_nontemporal_store(v4f{f.x, f.y, f.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
+    k1_epilogue<K>(pos, nrm, N, i, vi, l, dk, k, kstore, rho, tau, damp, cov, idx, fn, err);
+}
+
+// ------------------------------------------------------------------ anchored kNN (seeded iterations, K <= 32)
+// Every point keeps an ANCHOR: a position a it was searched at, the exact KA = 2K nearest snapshot points S of a
+// (alist, column-major [KA][N]) and D = the KA-th distance there (anc[i].w; < 0: none yet).  Every snapshot point
+// outside S is >= D from a, hence >= D - |q - a| from the current position q.  So when the kstore-th distance of q
+// over S is below D - |q - a| (with rounding margins), the kstore nearest of q over the WHOLE snapshot are the
+// kstore nearest over S, in the same (d², index) key order -- exact, with KA gathers and one sorting network
+// instead of a grid search.  Points move a few % of their k-th distance per iteration, so 1-3 % of the queries per
+// iteration fail the test (measured at 1M and 10M, tools/anchor_probe.py); they are appended to a redo list and
+// re-anchored at q by a full grid search (k_knn_redo_nvt1).  Anchors depend only on the snapshot, so they stay
+// valid across load() calls.
+static constexpr float kAnchorEps = 4e-6f;   // relative slack for the fp32 distances (each is within ~2 ulp)
+
+PCD_DEV bool anchor_holds(float d2k, Vec3 q, float4 a) {
+    const float dq = sqrtf(d2k) * (1.f + kAnchorEps);
+    const float delta = sqrtf(sq3(q - v3(a.x, a.y, a.z))) * (1.f + kAnchorEps);
+    return a.w >= 0.f && dq + delta < a.w * (1.f - kAnchorEps);
+}
+
+// One entry per failing lane, one atomic per wave.
+PCD_DEV void redo_append(bool fail, int64_t i, int32_t* __restrict__ redo, unsigned* __restrict__ cnt) {
+    const unsigned long long m = __ballot(fail);
+    if (m == 0ull) return;
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __ffsll((long long)m) - 1;
+    unsigned base = 0;
+    if (lane == leader) base = atomicAdd(cnt, (unsigned)__popcll(m));
+    base = __shfl(base, leader);
+    if (fail) redo[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+}
+
+template <int K, int KA>
+__global__ __launch_bounds__(256) void k_knn_anchor_nvt1(GridView g, const float4* __restrict__ pos,
+                                                          const float4* __restrict__ nrm, int64_t N, RowMap rm, int k,
+                                                          int kstore, float rho, float tau, float damp, Cover cov,
+                                                          const float4* __restrict__ anc,
+                                                          const int32_t* __restrict__ alist,
+                                                          int32_t* __restrict__ idx, float4* __restrict__ fn,
+                                                          int* __restrict__ err, int32_t* __restrict__ redo,
+                                                          unsigned* __restrict__ redo_cnt) {
+    static_assert(KA == 2 * K, "anchor lists hold twice the list cap");
+    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (t0 >= rm.nq) return;
+    const int64_t i = rm(t0);
+    const float4 p4 = pos[i];
+    const Vec3 vi = v3(p4.x, p4.y, p4.z);
+    const float4 a = anc[i];
+    unsigned long long c[KA];
+    uint32_t r[KA];
+#pragma unroll
+    for (int t = 0; t < KA; ++t) r[t] = (uint32_t)__builtin_nontemporal_load(alist + (int64_t)t * N + i);
+#ifdef PCD_EXP_NOGATHER   // experiment builds only (tools/ab_probe.sh): timing of the parts, results wrong
+#pragma unroll
+    for (int t = 0; t < KA; ++t) c[t] = ((unsigned long long)(r[t] * 7u) << 32) | r[t];
+#else
+#pragma unroll
+    for (int t = 0; t < KA; ++t) c[t] = cand_key<false>(vi, g.pts[min(r[t], (uint32_t)(N - 1))], r[t]);
+#endif
+#ifndef PCD_EXP_NOSORT
+    bitonic_sort<KA>(c);
+#endif
+    float dk = 0.f;
+#pragma unroll
+    for (int t = 0; t < KA; ++t)
+        if (t == kstore - 1) dk = __uint_as_float((unsigned)(c[t] >> 32));
+    const bool ok = anchor_holds(dk, vi, a);
+    redo_append(!ok, i, redo, redo_cnt);
+    if (!ok) return;
+    int l[K];
+#pragma unroll
+    for (int t = 0; t < K; ++t) l[t] = (int)(uint32_t)(c[t] & 0xFFFFFFFFull);
+    k1_epilogue<K>(pos, nrm, N, i, vi, l, dk, k, kstore, rho, tau, damp, cov, idx, fn, err);
+}
+
+// Re-anchor: the exact KA nearest at the current position, one query per WAVE (pcd_wknn.h), capped by the old
+// anchor list re-keyed here when there is one (KA distinct points: its largest key bounds the new KA-th key).
+// Writes the anchor, its list and the kstore-column kNN list; k_redo_nvt1 then runs the K1 epilogue per lane.
+// DENSE: every active row (no anchors yet); else the rows on the redo list.  Grid-stride over waves.
+template <int KA, bool DENSE>
+__global__ __launch_bounds__(256) void k_knn_redo_wave(GridView g, const float4* __restrict__ pos, int64_t N, RowMap rm,
+                                                        int kstore, float4* __restrict__ anc,
+                                                        int32_t* __restrict__ alist, int32_t* __restrict__ idx,
+                                                        const int32_t* __restrict__ redo,
+                                                        const unsigned* __restrict__ redo_cnt) {
+    __shared__ unsigned long long s_buf[4][kWaveSurv];
+    __shared__ WaveCells s_cells[4];
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    const int64_t cnt = DENSE ? rm.nq : (int64_t)*redo_cnt;
+    for (int64_t t0 = blockIdx.x * 4ll + wv; t0 < cnt; t0 += (int64_t)gridDim.x * 4) {
+        const int64_t i = DENSE ? rm(t0) : (int64_t)redo[t0];
+        const float4 p4 = pos[i];
+        const Vec3 q = v3(p4.x, p4.y, p4.z);
+        unsigned long long cap = kInfKey;
+        if (!DENSE && anc[i].w >= 0.f) {
+            unsigned long long c = 0ull;
+            if (lane < KA) {
+                const uint32_t r = (uint32_t)alist[(int64_t)lane * N + i];
+                c = cand_key<false>(q, g.pts[min(r, (uint32_t)(N - 1))], r);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const unsigned long long x = shfl_xor_u64(c, o);
+                c = x > c ? x : c;
+            }
+            cap = c + 1ull;
+        }
+        const unsigned long long top = wave_knn<KA>(g, q, cap, s_buf[wv], &s_cells[wv], lane);
+        const int32_t r = (int32_t)(uint32_t)(top & 0xFFFFFFFFull);
+        if (lane < KA) alist[(int64_t)lane * N + i] = r;
+        if (lane < kstore) idx[(int64_t)lane * N + i] = r;
+        // D: the KA-th distance (every other snapshot point is at least this far from the anchor)
+        if (lane == KA - 1) anc[i] = make_float4(q.x, q.y, q.z, sqrtf(__uint_as_float((unsigned)(top >> 32))));
+    }
+}
+
+// K1 epilogue for the re-anchored rows (lane per row, list from idx).
+template <int K, bool DENSE>
+__global__ __launch_bounds__(256) void k_redo_nvt1(GridView g, const float4* __restrict__ pos,
+                                                    const float4* __restrict__ nrm, int64_t N, RowMap rm, int k,
+                                                    int kstore, float rho, float tau, float damp, Cover cov,
+                                                    int32_t* __restrict__ idx, float4* __restrict__ fn,
+                                                    int* __restrict__ err, const int32_t* __restrict__ redo,
+                                                    const unsigned* __restrict__ redo_cnt) {
+    const int64_t cnt = DENSE ? rm.nq : (int64_t)*redo_cnt;
+    for (int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t0 < cnt; t0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = DENSE ? rm(t0) : (int64_t)redo[t0];
+        const float4 p4 = pos[i];
+        const Vec3 vi = v3(p4.x, p4.y, p4.z);
+        int l[K];
+        float dk = 0.f;
+#pragma unroll
+        for (int t = 0; t < K; ++t) {
+            l[t] = t < kstore ? idx[(int64_t)t * N + i] : (int)i;
+            if (t == kstore - 1) dk = dist2(vi, g.pts[min((uint32_t)l[t], (uint32_t)(N - 1))]);
+        }
+        k1_epilogue<K>(pos, nrm, N, i, vi, l, dk, k, kstore, rho, tau, damp, cov, idx, fn, err);
+    }
 }
 
 // K2: NVT2 on f_n -> classes + edge vectors.
@@ -292,6 +452,13 @@ struct pcd_denoiser {
     Cover cov{{1.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};  // disabled
     int seed_cols = 0;            // columns of idx holding a valid kNN list of the snapshot (0: none yet)
     bool seeding = true;          // use the stored list as an acceptance cap (pcd_denoiser_set_seeding)
+    // anchored kNN (list cap <= 32): anchors + their 2K-lists, the redo list of queries that failed the test
+    float4* anc = nullptr;
+    int32_t* alist = nullptr;
+    int32_t* redo = nullptr;
+    unsigned* redo_cnt = nullptr;
+    int anchor_ka = 0;            // KA of the stored anchors (0: none)
+    bool anchoring = true;        // anchored kNN for seeded searches (pcd_denoiser_set_anchoring)
     bool loaded = false, iterated = false;
     bool timing = false;
     std::vector<hipEvent_t> ev;
@@ -324,11 +491,65 @@ static bool phase_is_global(const pcd_denoise_params* p, int ph) {
     return p->phase_kind[ph] == PCD_STEP_FLAT || p->phase_kind[ph] == PCD_STEP_NEW;
 }
 
+// Anchored K1 (seeded, list cap K <= 32, KA = 2K): the anchor test for every active row, then a re-anchoring
+// grid search for the rows that failed it -- or for every row when there are no anchors (of this KA) yet.
+static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int K, hipStream_t st) {
+    const int64_t N = dn->n;
+    const RowMap rm = dn->rowmap();
+    const int kstore = std::max(p->k, p->k_update);
+    const int KA = 2 * K;
+    if (!dn->anc) {
+        if (hipMalloc(&dn->anc, N * sizeof(float4)) != hipSuccess ||
+            hipMalloc(&dn->alist, (int64_t)2 * knn_cap(dn->kcap) * N * sizeof(int32_t)) != hipSuccess ||
+            hipMalloc(&dn->redo, N * sizeof(int32_t)) != hipSuccess ||
+            hipMalloc(&dn->redo_cnt, sizeof(unsigned)) != hipSuccess)
+            return fail(PCD_ERR_OOM, "pcd_denoiser: anchor buffers");
+        dn->anchor_ka = 0;
+    }
+    const bool dense = dn->anchor_ka != KA;
+    if (dense) PCD_HIP(hipMemsetAsync(dn->anc, 0xFF, N * sizeof(float4), st));   // NaN radius: no anchor
+    const GridView gv = dn->g->view;
+    float4* P = dn->pos[dn->cur];
+    const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
+    const dim3 grd_redo((unsigned)std::min<int64_t>(cdiv(rm.nq, 256), 2048));
+    const dim3 grd_wave((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), dense ? 8192 : 2048));
+    PCD_HIP(hipMemsetAsync(dn->redo_cnt, 0, sizeof(unsigned), st));
+#define PCD_K1A(C)                                                                                                     \
+    case C:                                                                                                            \
+        if (dense) {                                                                                                   \
+            hipLaunchKernelGGL((k_knn_redo_wave<2 * C, true>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,    \
+                               dn->alist, dn->idx, dn->redo, dn->redo_cnt);                                            \
+            hipLaunchKernelGGL((k_redo_nvt1<C, true>), grd, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore, p->rho,   \
+                               p->tau, p->damp, dn->cov, dn->idx, dn->fn, dn->err, dn->redo, dn->redo_cnt);            \
+        } else {                                                                                                       \
+            hipLaunchKernelGGL((k_knn_anchor_nvt1<C, 2 * C>), grd, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore,    \
+                               p->rho, p->tau, p->damp, dn->cov, dn->anc, dn->alist, dn->idx, dn->fn, dn->err,         \
+                               dn->redo, dn->redo_cnt);                                                                \
+            hipLaunchKernelGGL((k_knn_redo_wave<2 * C, false>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,   \
+                               dn->alist, dn->idx, dn->redo, dn->redo_cnt);                                            \
+            hipLaunchKernelGGL((k_redo_nvt1<C, false>), grd_redo, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore,     \
+                               p->rho, p->tau, p->damp, dn->cov, dn->idx, dn->fn, dn->err, dn->redo, dn->redo_cnt);    \
+        }                                                                                                              \
+        break;
+    switch (K) {
+        PCD_K1A(8) PCD_K1A(16) PCD_K1A(32)
+        default: return fail(PCD_ERR_ARG, "unsupported k");
+    }
+#undef PCD_K1A
+    PCD_LAUNCH_CHECK();
+    dn->anchor_ka = KA;
+    dn->seed_cols = kstore;
+    return PCD_OK;
+}
+
 static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t st) {
     const int64_t N = dn->n;
     const RowMap rm = dn->rowmap();
     if (rm.nq == 0) return PCD_OK;
     const int kstore = std::max(p->k, p->k_update);
+    const int K = list_cap(p);
+    if (dn->seeding && dn->anchoring && K <= 32 && N >= 2 * K && knn_cap(dn->kcap) <= 32)
+        return stage_k1_anchored(dn, p, K, st);
     const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
     const GridView gv = dn->g->view;
     float4* P = dn->pos[dn->cur];
@@ -338,7 +559,7 @@ static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t s
         if (seed) hipLaunchKernelGGL((k_knn_nvt1<C, true>), grd, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore, p->rho, p->tau, p->damp, dn->cov, dn->idx, dn->fn, dn->err); \
         else hipLaunchKernelGGL((k_knn_nvt1<C, false>), grd, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore, p->rho, p->tau, p->damp, dn->cov, dn->idx, dn->fn, dn->err); \
         break;
-    switch (list_cap(p)) {
+    switch (K) {
         PCD_K1(8) PCD_K1(16) PCD_K1(32) PCD_K1(64)
         default: return fail(PCD_ERR_ARG, "unsupported k");
     }
@@ -467,6 +688,7 @@ int pcd_denoiser_destroy(pcd_denoiser* dn) {
     (void)hipFree(dn->pos[0]); (void)hipFree(dn->pos[1]); (void)hipFree(dn->nrm); (void)hipFree(dn->fn);
     (void)hipFree(dn->edge); (void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part);
     (void)hipFree(dn->red); (void)hipFree(dn->gscal); (void)hipFree(dn->err);
+    (void)hipFree(dn->anc); (void)hipFree(dn->alist); (void)hipFree(dn->redo); (void)hipFree(dn->redo_cnt);
     for (auto e : dn->ev) (void)hipEventDestroy(e);
     delete dn;
     return PCD_OK;
@@ -565,6 +787,13 @@ int pcd_denoiser_check(pcd_denoiser* dn, void* stream) {
 int pcd_denoiser_reset_seed(pcd_denoiser* dn) {
     PCD_CHECK_ARG(dn != nullptr, "null denoiser");
     dn->seed_cols = 0;
+    dn->anchor_ka = 0;
+    return PCD_OK;
+}
+
+int pcd_denoiser_set_anchoring(pcd_denoiser* dn, int enable) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    dn->anchoring = enable != 0;
     return PCD_OK;
 }
 

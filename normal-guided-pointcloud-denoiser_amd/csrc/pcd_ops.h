@@ -20,11 +20,19 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho) {
         const int64_t j = nb(t);
         const Vec3 vj = pos(j), nj = nrm(j);
         const Vec3 dv = vj - vi;
+#if defined(PCD_EXP_NOVOTE)
+        const bool w = dv.x > 0.f;
+#else
         const float den = fmaxf(sqrtf(sq3(dv)), 1e-12f);
         const Vec3 dn = v3(dv.x / den, dv.y / den, dv.z / den);
         float c = dot3(dn, nj);
         c = fabsf(fminf(fmaxf(c, -1.f), 1.f));
+#if defined(PCD_EXP_NOACOS)
+        const bool w = c < rho;
+#else
         const bool w = acosf(c) > rho;
+#endif
+#endif
         const float o00 = nj.x * nj.x, o01 = nj.x * nj.y, o02 = nj.x * nj.z;
         const float o11 = nj.y * nj.y, o12 = nj.y * nj.z, o22 = nj.z * nj.z;
         u00 += o00; u01 += o01; u02 += o02; u11 += o11; u12 += o12; u22 += o22;

@@ -1,0 +1,223 @@
+// Wave-cooperative exact kNN: ONE query per wave64 (the re-anchoring search of the anchored kNN, denoise.hip).
+//
+// The lane-per-query searches (pcd_knn.h) keep a sorted top-K in each lane's registers; at K = 64 that list is 128
+// VGPRs and every accepted candidate runs a 64-step select chain, so a sparse set of queries (the 1-3 % that fail
+// the anchor test) runs at 2 waves/SIMD on long serial chains.  Here the 64 lanes split one query's work instead:
+//   1. the cells of the box [q - r, q + r] (r = sqrt of the acceptance cap) are dealt one per lane, pruned by
+//      box distance, probed in the hash table in parallel, and their point counts wave-scanned;
+//   2. the flattened candidate rows are dealt one per lane per pass (cell found by a binary search of the scan in
+//      LDS); a key (d² bits << 32 | rank) below the cap is appended to the wave's LDS survivor buffer with one
+//      ballot-compaction per pass;
+//   3. the survivors (a few more than K when the cap is tight) are bitonic-sorted across the wave in registers
+//      (4 keys per lane, slot-major: key e lives in lane e % 64, slot e / 64), so lane t ends with the t-th key.
+// A full buffer is reduced in place (sort, keep the K best, tighten the cap), so any cap >= the true K-th key is
+// exact; without a finite cap the search first runs over growing Chebyshev blocks to find one.
+// Keys and their order are bit-identical to the lane searches: same fp32 (q-c)² and the same tie-break by rank.
+#pragma once
+#include "pcd_knn.h"
+
+namespace pcd {
+
+static constexpr int kWaveSurv = 256;   // survivor slots per wave (4 per lane)
+
+PCD_DEV void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+PCD_DEV unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+    const unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+    return (unsigned long long)(unsigned)__shfl_xor((int)lo, m) |
+           ((unsigned long long)(unsigned)__shfl_xor((int)hi, m) << 32);
+}
+
+// Ascending bitonic sort of the 64*M keys v[s] (element e = s*64 + lane) across the wave.
+template <int M>
+PCD_DEV void wave_bitonic_sort(unsigned long long (&v)[M], int lane) {
+    constexpr int NT = 64 * M;
+#pragma unroll
+    for (int size = 2; size <= NT; size <<= 1) {
+#pragma unroll
+        for (int stride = size / 2; stride > 0; stride >>= 1) {
+            if (stride >= 64) {              // partner in another slot of the same lane
+                const int ss = stride / 64;
+#pragma unroll
+                for (int s = 0; s < M; ++s) {
+                    if ((s & ss) == 0) {
+                        const int e = s * 64 + lane;
+                        const bool asc = (e & size) == 0;
+                        unsigned long long& a = v[s];
+                        unsigned long long& b = v[s + ss];
+                        const bool sw = asc ? (b < a) : (a < b);
+                        const unsigned long long lo = sw ? b : a;
+                        b = sw ? a : b;
+                        a = lo;
+                    }
+                }
+            } else {                         // partner lane ^ stride, same slot
+#pragma unroll
+                for (int s = 0; s < M; ++s) {
+                    const int e = s * 64 + lane;
+                    const bool asc = (e & size) == 0;
+                    const bool lower = (lane & stride) == 0;
+                    const unsigned long long o = shfl_xor_u64(v[s], stride);
+                    const unsigned long long mn = o < v[s] ? o : v[s];
+                    const unsigned long long mx = o < v[s] ? v[s] : o;
+                    v[s] = (lower == asc) ? mn : mx;
+                }
+            }
+        }
+    }
+}
+
+// Sort the cnt (<= kWaveSurv) survivors of buf; on return lane t's `top` is the t-th smallest key (kInfKey pad).
+// If keep > 0, the keep smallest are written back to buf[0..keep) and the count returned.
+PCD_DEV unsigned long long wave_sort_survivors(unsigned long long* buf, int cnt, int lane, int keep, int& kept) {
+    unsigned long long top;
+    if (cnt <= 64) {
+        unsigned long long v[1] = {lane < cnt ? buf[lane] : kInfKey};
+        wave_bitonic_sort<1>(v, lane);
+        top = v[0];
+    } else if (cnt <= 128) {
+        unsigned long long v[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) v[s] = s * 64 + lane < cnt ? buf[s * 64 + lane] : kInfKey;
+        wave_bitonic_sort<2>(v, lane);
+        top = v[0];
+    } else {
+        unsigned long long v[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) v[s] = s * 64 + lane < cnt ? buf[s * 64 + lane] : kInfKey;
+        wave_bitonic_sort<4>(v, lane);
+        top = v[0];
+    }
+    kept = 0;
+    if (keep > 0) {
+        wave_sync();
+        const int n = cnt < keep ? cnt : keep;
+        if (lane < n) buf[lane] = top;
+        kept = n;
+        wave_sync();
+    }
+    return top;
+}
+
+struct WaveCells {          // per-wave LDS scratch for one chunk of <= 64 cells
+    uint32_t start[64];
+    uint32_t end_excl[64];  // inclusive scan of the counts (flattened candidate end of each cell)
+};
+
+// Scan the cells of box [lo, hi] (cell coords), appending keys < cap to buf.  cap may tighten (buffer reduce).
+template <int K>
+PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int hi[3], unsigned long long& cap,
+                           unsigned long long* buf, int& cnt, WaveCells* wc, int lane) {
+    const int ex = hi[0] - lo[0] + 1, ey = hi[1] - lo[1] + 1, ez = hi[2] - lo[2] + 1;
+    const int64_t nc = (int64_t)ex * ey * ez;
+    for (int64_t base = 0; base < nc; base += 64) {
+        // 1. one cell per lane: prune by box distance, probe, count
+        uint32_t s = 0, e = 0;
+        const int64_t ci = base + lane;
+        if (ci < nc) {
+            const int cx = lo[0] + (int)(ci % ex), cy = lo[1] + (int)((ci / ex) % ey), cz = lo[2] + (int)(ci / ((int64_t)ex * ey));
+            const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
+            const float gx = axis_gap(q.x, lx, lx + g.h), gy = axis_gap(q.y, ly, ly + g.h), gz = axis_gap(q.z, lz, lz + g.h);
+            const float kth = __uint_as_float((unsigned)(cap >> 32));
+            if (gx * gx + gy * gy + gz * gz <= kth * 1.00001f + 1e-30f) {
+                if (!cell_range(g, cx, cy, cz, s, e)) s = e = 0;
+            }
+        }
+        uint32_t incl = e - s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
+            if (lane >= o) incl += t;
+        }
+        const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+        if (total == 0) continue;
+        wc->start[lane] = s;
+        wc->end_excl[lane] = incl;
+        wave_sync();
+        // 2. flattened candidates, one per lane per pass
+        for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+            if (cnt > kWaveSurv - 64) {      // make room: keep the K best, tighten the cap
+                int kept;
+                const unsigned long long top = wave_sort_survivors(buf, cnt, lane, K, kept);
+                const unsigned long long kth_key = __shfl(top, K - 1);
+                if (kept == K && kth_key + 1ull < cap) cap = kth_key + 1ull;
+                cnt = kept;
+            }
+            const uint32_t j = j0 + lane;
+            bool pass = false;
+            unsigned long long key = 0;
+            if (j < total) {
+                int a = 0, b = 63;           // first cell with end_excl > j
+                while (a < b) {
+                    const int m = (a + b) >> 1;
+                    if (wc->end_excl[m] > j) b = m; else a = m + 1;
+                }
+                const uint32_t r = wc->start[a] + (j - (a ? wc->end_excl[a - 1] : 0u));
+                key = cand_key<false>(q, g.pts[r], r);
+                pass = key < cap;
+            }
+            const unsigned long long m = __ballot(pass);
+            if (pass) buf[cnt + __popcll(m & ((1ull << lane) - 1ull))] = key;
+            cnt += __popcll(m);
+            wave_sync();
+        }
+    }
+}
+
+PCD_DEV void cell_box(const GridView& g, Vec3 q, float r, int lo[3], int hi[3]) {
+    const float qa[3] = {q.x, q.y, q.z}, o[3] = {g.ox, g.oy, g.oz};
+    const int dm[3] = {g.dx, g.dy, g.dz};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = min(max(cell_coord(qa[a] - r, o[a], g.inv_h), 0), dm[a] - 1);
+        hi[a] = min(max(cell_coord(qa[a] + r, o[a], g.inv_h), 0), dm[a] - 1);
+    }
+}
+
+// Exact top-K (K <= 64) of the snapshot for q; returns lane t's key t.  cap: kInfKey or a bound > the true K-th
+// key.  Requires K <= g.n.  buf: the wave's kWaveSurv-key LDS buffer; wc: its cell scratch.
+template <int K>
+PCD_DEV unsigned long long wave_knn(const GridView& g, Vec3 q, unsigned long long cap, unsigned long long* buf,
+                                    WaveCells* wc, int lane) {
+    static_assert(K <= 64, "one key per lane");
+    int cnt = 0, lo[3], hi[3];
+    const int c[3] = {min(max(cell_coord(q.x, g.ox, g.inv_h), 0), g.dx - 1),
+                      min(max(cell_coord(q.y, g.oy, g.inv_h), 0), g.dy - 1),
+                      min(max(cell_coord(q.z, g.oz, g.inv_h), 0), g.dz - 1)};
+    if (cap == kInfKey) {
+        // no bound yet: Chebyshev blocks of growing radius until they hold K points; their K-th key bounds it
+        for (int R = 1;; R = R * 2) {
+            const int dm[3] = {g.dx, g.dy, g.dz};
+            bool all = true;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = max(c[a] - R, 0);
+                hi[a] = min(c[a] + R, dm[a] - 1);
+                all = all && lo[a] == 0 && hi[a] == dm[a] - 1;
+            }
+            cnt = 0;
+            unsigned long long cp = kInfKey;
+            wave_scan_box<K>(g, q, lo, hi, cp, buf, cnt, wc, lane);
+            if (cnt >= K || all) {
+                int kept;
+                const unsigned long long top = wave_sort_survivors(buf, cnt, lane, 0, kept);
+                const unsigned long long kth_key = __shfl(top, K - 1);
+                if (all) return top;          // the whole grid was scanned: exact as it stands
+                cap = kth_key + 1ull;
+                break;
+            }
+        }
+        cnt = 0;
+    }
+    const float r = sqrtf(__uint_as_float((unsigned)(cap >> 32))) * 1.0001f + 1e-30f;
+    cell_box(g, q, r, lo, hi);
+    wave_scan_box<K>(g, q, lo, hi, cap, buf, cnt, wc, lane);
+    int kept;
+    return wave_sort_survivors(buf, cnt, lane, 0, kept);
+}
+
+}  // namespace pcd

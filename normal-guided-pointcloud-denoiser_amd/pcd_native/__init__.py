@@ -69,6 +69,7 @@ _SIGS = {
     "pcd_denoiser_set_timing": (c_int, [c_void_p, c_int]),
     "pcd_denoiser_reset_seed": (c_int, [c_void_p]),
     "pcd_denoiser_set_seeding": (c_int, [c_void_p, c_int]),
+    "pcd_denoiser_set_anchoring": (c_int, [c_void_p, c_int]),
     "pcd_denoiser_check": (c_int, [c_void_p, c_void_p]),
     "pcd_denoiser_set_rows": (c_int, [c_void_p, c_void_p, c_int64]),
     "pcd_denoiser_set_coverage": (c_int, [c_void_p, c_void_p, c_void_p]),
@@ -245,6 +246,9 @@ class FusedDenoiser:
 
     def set_seeding(self, enable=True):
         check(lib().pcd_denoiser_set_seeding(self.handle, int(bool(enable))), "pcd_denoiser_set_seeding")
+
+    def set_anchoring(self, enable=True):
+        check(lib().pcd_denoiser_set_anchoring(self.handle, int(bool(enable))), "pcd_denoiser_set_anchoring")
 
     def reset_seed(self):
         check(lib().pcd_denoiser_reset_seed(self.handle), "pcd_denoiser_reset_seed")

@@ -260,10 +260,11 @@ def test_fused_iteration_matches_reference(fan, gpu):
     assert np.percentile(dev, 99) < 3e-4 and np.median(dev) < 1e-6
 
 
-@pytest.mark.parametrize("k", [8, 16, 32, 64])
-def test_seeded_knn_matches_unseeded(golden, gpu, k):
-    """With seeding on, iterations >= 2 cap the search at the previous list's largest key; the result must be
-    bit-identical to a fresh unseeded search -- checked on the full denoise state after 3 iterations."""
+@pytest.mark.parametrize("k,anchoring", [(8, True), (16, True), (32, True), (64, True), (16, False), (32, False)])
+def test_seeded_knn_matches_unseeded(golden, gpu, k, anchoring):
+    """With seeding on, iterations >= 2 either certify each point's anchored 2K-list (anchoring, K <= 32) or cap the
+    grid search at the previous list's largest key; the result must be bit-identical to a fresh unseeded search --
+    checked on the full denoise state after 4 iterations."""
     fan = golden("fandisk_k32")
     outs = []
     for reset in (False, True):
@@ -272,8 +273,9 @@ def test_seeded_knn_matches_unseeded(golden, gpu, k):
         fused = proc._fused_for(max(k, 8))
         fused.load(proc.graph.pos, proc.graph.n)
         fused.set_seeding(not reset)
+        fused.set_anchoring(anchoring)
         params = nat.make_params(k=k, k_update=8, d=float(fan["d"]))
-        for _ in range(3):
+        for _ in range(4):
             if reset:
                 fused.reset_seed()
             fused.iterate(params, 1)
@@ -281,6 +283,57 @@ def test_seeded_knn_matches_unseeded(golden, gpu, k):
         pos = torch.empty((N, 3), device=gpu); n = torch.empty((N, 3), device=gpu)
         fused.store(pos, n)
         outs.append((pos.cpu().numpy(), n.cpu().numpy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+def test_anchors_survive_reload(golden, gpu):
+    """Anchors depend only on the snapshot: after load() of a moved state, the anchored search must give the same
+    lists (and so the same iteration) as a denoiser that has never anchored."""
+    fan = golden("fandisk_k32")
+    pc = Pointcloud(T(fan["pos0"], gpu).clone(), T(fan["n0"], gpu).clone())
+    proc = Processor(pc, k_hint=32)
+    params = nat.make_params(k=32, k_update=8, d=float(fan["d"]))
+    a = proc._fused_for(32)
+    a.load(proc.graph.pos, proc.graph.n)
+    a.iterate(params, 3)
+    N = len(fan["pos0"])
+    pos = torch.empty((N, 3), device=gpu); n = torch.empty((N, 3), device=gpu)
+    a.store(pos, n)
+    outs = []
+    for fused in (a, nat.FusedDenoiser(proc.selector.grid, 32)):
+        fused.load(pos, n)                   # anchored (a) vs fresh (dense re-anchoring) from the same state
+        fused.iterate(params, 2)
+        p2 = torch.empty((N, 3), device=gpu); n2 = torch.empty((N, 3), device=gpu)
+        fused.store(p2, n2)
+        outs.append((p2.cpu().numpy(), n2.cpu().numpy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+def test_wave_knn_far_queries(gpu):
+    """Queries far outside the snapshot (huge k-balls, many cells, buffer reductions) through the anchored path:
+    lists must equal the lane search's (unseeded) exactly."""
+    g = torch.Generator().manual_seed(5)
+    snap = torch.rand((20000, 3), generator=g) * torch.tensor([1.0, 1.0, 0.02])
+    nrm = torch.nn.functional.normalize(torch.randn((20000, 3), generator=g), dim=1)
+    outs = []
+    for seeding in (True, False):
+        pc = Pointcloud(snap.clone().to(gpu), nrm.clone().to(gpu))
+        proc = Processor(pc, k_hint=32)
+        fused = proc._fused_for(32)
+        fused.load(proc.graph.pos, proc.graph.n)
+        fused.set_seeding(seeding)
+        params = nat.make_params(k=32, k_update=8, d=0.05)
+        fused.iterate(params, 1)                      # anchors at the snapshot
+        moved = snap.clone()
+        moved[::7, 2] += 0.3                          # far off the sheet: every cap is loose
+        moved[1::7, :2] += 0.02
+        fused.load(moved.to(gpu), nrm.to(gpu))
+        fused.iterate(params, 1)
+        p = torch.empty((20000, 3), device=gpu); n = torch.empty((20000, 3), device=gpu)
+        fused.store(p, n)
+        outs.append((p.cpu().numpy(), n.cpu().numpy()))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
 
