@@ -48,6 +48,14 @@ def knn_cap(k):
     return 8 if k <= 8 else 16 if k <= 16 else 32 if k <= 32 else 64
 
 
+def k1_kernels(k, ku, seeding, anchoring):
+    """Kernels of the K1 stage (kNN + NVT1) as pcd_denoiser_iterate launches them in a timed (seeded) step."""
+    c = knn_cap(max(k, ku))
+    if seeding and anchoring and c <= 32:
+        return [f"k_knn_anchor<{c}, {2 * c}>", f"k_knn_redo_wave<{2 * c}, false>", f"k_nvt1<{c}>"]
+    return [f"k_knn_nvt1<{c}, {'true' if seeding else 'false'}>"]
+
+
 def b_alg_iteration(k, ku):
     """Algorithmic bytes / point / iteration: 148 + 72k + 60k_u."""
     return 148 + 72 * k + 60 * ku
@@ -105,7 +113,8 @@ def main():
                     help="run every kNN search unseeded (the seeded search is the default; identical results)")
     ap.add_argument("--no-anchoring", dest="anchoring", action="store_false",
                     help="seeded searches without anchors (capped grid search every iteration; identical results)")
-    ap.add_argument("--profile-steps", type=int, default=5, help="extra per-kernel timed iterations (HIP events)")
+    ap.add_argument("--profile-steps", type=int, default=5,
+                    help="slab mode: extra per-stage timed iterations after the timed region (torch events)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: independent clouds per rank instead of spatial slabs of one global cloud")
     args = ap.parse_args()
@@ -153,8 +162,18 @@ def main():
         params = nat.make_params(k=args.k, k_update=args.k_update, d=d)
         step = lambda: fused.iterate(params, 1)  # noqa: E731
 
-    for _ in range(args.warmup):
-        step()
+    first_ms = None
+    for w in range(args.warmup):
+        if w == 0:                 # iteration 1 builds every anchor (dense search): reported on its own
+            torch.cuda.synchronize()
+            tf = time.perf_counter()
+            step()
+            torch.cuda.synchronize()
+            first_ms = (time.perf_counter() - tf) * 1e3
+        else:
+            step()
+    if mode != "slab":
+        fused.set_timing(True)     # per-stage HIP events on the launch stream, every timed iteration
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -184,30 +203,25 @@ def main():
             kernel_ms = {key: round(float(np.mean([x[key] for x in ks])), 4) for key in ks[0]}
             knn_ms = kernel_ms["knn_nvt1"]
     else:
-        fused.set_timing(True)
-        slots = []
-        for _ in range(args.profile_steps):
-            fused.iterate(params, 1)
-            slots.append(fused.timing())
+        slots = fused.timing()      # averages over exactly the timed iterations
         fused.set_timing(False)
-        slots = np.asarray(slots)
-        if len(slots):
-            knn_ms = float(np.mean(slots[:, 0]))
+        if slots:
+            knn_ms = float(slots[0])
             names = ["knn_nvt1", "nvt2", "flat_phase", "edge_phase", "corner_phase"]
-            kernel_ms = {names[i]: round(float(np.mean(slots[:, i])), 4) for i in range(min(slots.shape[1], 5))}
+            kernel_ms = {names[i]: round(float(slots[i]), 4) for i in range(min(len(slots), 5))}
 
     k1_points = sd.owned_global.numel() if mode == "slab" else args.points
     k1_bytes = b_alg_knn_nvt1(args.k) * k1_points
     achieved = k1_bytes / (knn_ms / 1e3) / 1e9 if knn_ms == knn_ms else None
+    k1_names = k1_kernels(args.k, args.k_update, args.seeding, args.anchoring)
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile) and mode != "slab":
         try:
             tj = json.load(open(tfile))
             if tj.get("points") == args.points and tj.get("k") == args.k:
-                for e in tj["kernels"].get(f"k_knn_nvt1<{knn_cap(max(args.k, args.k_update))}, "
-                                           f"{'true' if args.seeding else 'false'}>", []):
-                    traffic = e.get("hbm_bytes_per_launch")
+                per = [tj["kernels"][nm][0]["hbm_bytes_per_launch"] for nm in k1_names]
+                traffic = float(sum(per))
         except Exception:
             traffic = None
     iter_alg = b_alg_iteration(args.k, args.k_update) * args.points
@@ -234,12 +248,13 @@ def main():
                    "parallelism": {"single": "single", "replicas": f"replicas x{world}",
                                    "slab": f"spatial slabs x{world}"}[mode]},
         "iterations_per_sec": round(1e3 / ms_per_step, 2),
+        "first_iteration_ms": round(first_ms, 3) if first_ms is not None else None,
         "kernel_ms": kernel_ms,
         "iteration_roofline": {"bound": "hbm", "alg_bytes_per_point": b_alg_iteration(args.k, args.k_update),
                                "achieved": round(iter_alg / (ms_per_step / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
                                "unit": "GB/s",
                                "frac": round(iter_alg / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
-        "roofline": {"kernel": "k_knn_nvt1", "bound": "hbm",
+        "roofline": {"kernel": "K1 stage (kNN + NVT1): " + " + ".join(k1_names), "bound": "hbm",
                      "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                      "traffic": traffic, "alg_bytes_per_launch": k1_bytes, "avg_launch_ms": round(knn_ms, 4)},

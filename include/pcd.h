@@ -161,7 +161,11 @@ int pcd_denoiser_reset_seed(pcd_denoiser* dn);
  * k-NN (no grid search); the few queries that fail are re-anchored by a full grid search.  Same results (tested
  * bitwise).  Anchors depend only on the snapshot: they survive load(); reset_seed drops them. */
 int pcd_denoiser_set_anchoring(pcd_denoiser* dn, int enable);
-/* Profiling aid: elapsed ms of each kernel class in the last iterate() when timing was enabled. */
+/* Diagnostics: rows re-anchored by the last anchored kNN stage (-1: none ran).  Synchronises `stream`. */
+int pcd_denoiser_anchor_stats(pcd_denoiser* dn, int64_t* redo_rows, void* stream);
+/* Profiling aid: with timing enabled, every iteration (up to 256) records HIP events on its stream between the
+ * stages; get_timing returns each stage's elapsed ms AVERAGED over the iterations recorded since set_timing or
+ * the previous get_timing (slots: kNN+NVT1, NVT2, phase 0, phase 1, phase 2, finish, -), then starts over. */
 int pcd_denoiser_set_timing(pcd_denoiser* dn, int enable);
 int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n_written);
 /* Device error word -> status: PCD_ERR_STATE if a kNN list held an invalid entry or (spatial slabs) a query's

@@ -17,7 +17,10 @@
 // exchange between stages (pcd_denoiser_pack/unpack), and the global flat centre / delta reductions are exposed as
 // separate stages so the caller can all-reduce them (pcd_denoiser_stage).  pcd_denoiser_iterate is the same stage
 // sequence with no exchange.
+#include <cstring>
 #include <vector>
+
+#include <rocprim/rocprim.hpp>
 
 #include "pcd_knn.h"
 #include "pcd_ops.h"
@@ -76,6 +79,7 @@ struct RowMap {
 // the slab widened by the halo).  Disabled when lo > hi on axis 0.
 struct Cover {
     float lo[3], hi[3];
+    PCD_DEV bool enabled() const { return !(lo[0] > hi[0]); }
     PCD_DEV bool holds(Vec3 q, float d2) const {
         if (lo[0] > hi[0]) return true;
         const float r = sqrtf(d2) * 1.000001f + 1e-30f;
@@ -186,27 +190,22 @@ PCD_DEV bool anchor_holds(float d2k, Vec3 q, float4 a) {
     return a.w >= 0.f && dq + delta < a.w * (1.f - kAnchorEps);
 }
 
-// One entry per failing lane, one atomic per wave.
-PCD_DEV void redo_append(bool fail, int64_t i, int32_t* __restrict__ redo, unsigned* __restrict__ cnt) {
-    const unsigned long long m = __ballot(fail);
-    if (m == 0ull) return;
-    const int lane = (int)(threadIdx.x & 63);
-    const int leader = __ffsll((long long)m) - 1;
-    unsigned base = 0;
-    if (lane == leader) base = atomicAdd(cnt, (unsigned)__popcll(m));
-    base = __shfl(base, leader);
-    if (fail) redo[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+// Acceptance cap for re-anchoring at q: the KA anchor points are within D of a, hence within D + |q - a| of q, so
+// the KA-th key at q is below this bound (rounding margin included).  No list read: the redo rows are sparse, and
+// their column-major list rows would cost a cache line per entry.
+PCD_DEV unsigned long long anchor_cap(Vec3 q, float4 a) {
+    const float R = (a.w + sqrtf(sq3(q - v3(a.x, a.y, a.z)))) * (1.f + 1e-5f) + 1e-30f;
+    const float R2 = R * R * (1.f + 1e-5f);
+    return ((unsigned long long)__float_as_uint(R2) << 32) | 0xFFFFFFFFull;
 }
 
+// The anchor test for every active row; certified rows get their kstore-column list, the others go to the redo
+// list.  (NVT1 runs afterwards over all rows, k_nvt1.)
 template <int K, int KA>
-__global__ __launch_bounds__(256) void k_knn_anchor_nvt1(GridView g, const float4* __restrict__ pos,
-                                                          const float4* __restrict__ nrm, int64_t N, RowMap rm, int k,
-                                                          int kstore, float rho, float tau, float damp, Cover cov,
-                                                          const float4* __restrict__ anc,
-                                                          const int32_t* __restrict__ alist,
-                                                          int32_t* __restrict__ idx, float4* __restrict__ fn,
-                                                          int* __restrict__ err, int32_t* __restrict__ redo,
-                                                          unsigned* __restrict__ redo_cnt) {
+__global__ __launch_bounds__(256) void k_knn_anchor(GridView g, const float4* __restrict__ pos, int64_t N, RowMap rm,
+                                                     int kstore, const float4* __restrict__ anc,
+                                                     const int32_t* __restrict__ alist, int32_t* __restrict__ idx,
+                                                     uint8_t* __restrict__ fail) {
     static_assert(KA == 2 * K, "anchor lists hold twice the list cap");
     const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     if (t0 >= rm.nq) return;
@@ -218,32 +217,59 @@ __global__ __launch_bounds__(256) void k_knn_anchor_nvt1(GridView g, const float
     uint32_t r[KA];
 #pragma unroll
     for (int t = 0; t < KA; ++t) r[t] = (uint32_t)__builtin_nontemporal_load(alist + (int64_t)t * N + i);
-#ifdef PCD_EXP_NOGATHER   // experiment builds only (tools/ab_probe.sh): timing of the parts, results wrong
-#pragma unroll
-    for (int t = 0; t < KA; ++t) c[t] = ((unsigned long long)(r[t] * 7u) << 32) | r[t];
-#else
 #pragma unroll
     for (int t = 0; t < KA; ++t) c[t] = cand_key<false>(vi, g.pts[min(r[t], (uint32_t)(N - 1))], r[t]);
-#endif
-#ifndef PCD_EXP_NOSORT
     bitonic_sort<KA>(c);
-#endif
     float dk = 0.f;
 #pragma unroll
     for (int t = 0; t < KA; ++t)
         if (t == kstore - 1) dk = __uint_as_float((unsigned)(c[t] >> 32));
     const bool ok = anchor_holds(dk, vi, a);
-    redo_append(!ok, i, redo, redo_cnt);
+    fail[t0] = ok ? 0 : 1;            // -> ordered redo list (rocprim::select), so redo rows stay in spatial order
     if (!ok) return;
-    int l[K];
 #pragma unroll
-    for (int t = 0; t < K; ++t) l[t] = (int)(uint32_t)(c[t] & 0xFFFFFFFFull);
-    k1_epilogue<K>(pos, nrm, N, i, vi, l, dk, k, kstore, rho, tau, damp, cov, idx, fn, err);
+    for (int t = 0; t < K; ++t)
+        if (t < kstore) __builtin_nontemporal_store((int32_t)(uint32_t)(c[t] & 0xFFFFFFFFull), idx + (int64_t)t * N + i);
+}
+
+// NVT1 + eigh + VU smoothing over the stored lists (lane per active row); checks every list entry and, for
+// spatial slabs, that the kstore-ball stays inside the local snapshot.
+template <int K>
+__global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
+                                               const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
+                                               int kstore, float rho, float tau, float damp, Cover cov,
+                                               float4* __restrict__ fn, int* __restrict__ err) {
+    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (t0 >= rm.nq) return;
+    const int64_t i = rm(t0);
+    const float4 p4 = pos[i];
+    const Vec3 vi = v3(p4.x, p4.y, p4.z);
+    int l[K];
+    bool bad = false;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+        l[t] = t < kstore ? idx[(int64_t)t * N + i] : (int)i;
+        if ((uint32_t)l[t] >= (uint32_t)N) { bad = true; l[t] = (int)i; }
+    }
+    if (bad) atomicOr(err, 1);
+    if (cov.enabled()) {
+        float dk = 0.f;
+#pragma unroll
+        for (int t = 0; t < K; ++t)
+            if (t == kstore - 1) dk = dist2(vi, g.pts[l[t]]);
+        if (!cov.holds(vi, dk)) atomicOr(err, 2);
+    }
+    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho);
+    float w[3], V[3][3];
+    eigh3(T, w, V);
+    const float4 n4 = nrm[i];
+    const Vec3 f = vu_smooth(w, V, v3(n4.x, n4.y, n4.z), tau, damp);
+    __builtin_nontemporal_store(v4f{f.x, f.y, f.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
 }
 
 // Re-anchor: the exact KA nearest at the current position, one query per WAVE (pcd_wknn.h), capped by the old
 // anchor list re-keyed here when there is one (KA distinct points: its largest key bounds the new KA-th key).
-// Writes the anchor, its list and the kstore-column kNN list; k_redo_nvt1 then runs the K1 epilogue per lane.
+// Writes the anchor, its list and the kstore-column kNN list.
 // DENSE: every active row (no anchors yet); else the rows on the redo list.  Grid-stride over waves.
 template <int KA, bool DENSE>
 __global__ __launch_bounds__(256) void k_knn_redo_wave(GridView g, const float4* __restrict__ pos, int64_t N, RowMap rm,
@@ -255,23 +281,16 @@ __global__ __launch_bounds__(256) void k_knn_redo_wave(GridView g, const float4*
     __shared__ WaveCells s_cells[4];
     const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
     const int64_t cnt = DENSE ? rm.nq : (int64_t)*redo_cnt;
-    for (int64_t t0 = blockIdx.x * 4ll + wv; t0 < cnt; t0 += (int64_t)gridDim.x * 4) {
+    // consecutive redo rows (spatial neighbours) -> consecutive logical blocks -> the same XCD's L2
+    const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
+    for (int64_t t0 = lb * 4 + wv; t0 < cnt; t0 += (int64_t)gridDim.x * 4) {
         const int64_t i = DENSE ? rm(t0) : (int64_t)redo[t0];
         const float4 p4 = pos[i];
         const Vec3 q = v3(p4.x, p4.y, p4.z);
         unsigned long long cap = kInfKey;
-        if (!DENSE && anc[i].w >= 0.f) {
-            unsigned long long c = 0ull;
-            if (lane < KA) {
-                const uint32_t r = (uint32_t)alist[(int64_t)lane * N + i];
-                c = cand_key<false>(q, g.pts[min(r, (uint32_t)(N - 1))], r);
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const unsigned long long x = shfl_xor_u64(c, o);
-                c = x > c ? x : c;
-            }
-            cap = c + 1ull;
+        if (!DENSE) {
+            const float4 a = anc[i];
+            if (a.w >= 0.f) cap = anchor_cap(q, a);
         }
         const unsigned long long top = wave_knn<KA>(g, q, cap, s_buf[wv], &s_cells[wv], lane);
         const int32_t r = (int32_t)(uint32_t)(top & 0xFFFFFFFFull);
@@ -279,30 +298,6 @@ __global__ __launch_bounds__(256) void k_knn_redo_wave(GridView g, const float4*
         if (lane < kstore) idx[(int64_t)lane * N + i] = r;
         // D: the KA-th distance (every other snapshot point is at least this far from the anchor)
         if (lane == KA - 1) anc[i] = make_float4(q.x, q.y, q.z, sqrtf(__uint_as_float((unsigned)(top >> 32))));
-    }
-}
-
-// K1 epilogue for the re-anchored rows (lane per row, list from idx).
-template <int K, bool DENSE>
-__global__ __launch_bounds__(256) void k_redo_nvt1(GridView g, const float4* __restrict__ pos,
-                                                    const float4* __restrict__ nrm, int64_t N, RowMap rm, int k,
-                                                    int kstore, float rho, float tau, float damp, Cover cov,
-                                                    int32_t* __restrict__ idx, float4* __restrict__ fn,
-                                                    int* __restrict__ err, const int32_t* __restrict__ redo,
-                                                    const unsigned* __restrict__ redo_cnt) {
-    const int64_t cnt = DENSE ? rm.nq : (int64_t)*redo_cnt;
-    for (int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t0 < cnt; t0 += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = DENSE ? rm(t0) : (int64_t)redo[t0];
-        const float4 p4 = pos[i];
-        const Vec3 vi = v3(p4.x, p4.y, p4.z);
-        int l[K];
-        float dk = 0.f;
-#pragma unroll
-        for (int t = 0; t < K; ++t) {
-            l[t] = t < kstore ? idx[(int64_t)t * N + i] : (int)i;
-            if (t == kstore - 1) dk = dist2(vi, g.pts[min((uint32_t)l[t], (uint32_t)(N - 1))]);
-        }
-        k1_epilogue<K>(pos, nrm, N, i, vi, l, dk, k, kstore, rho, tau, damp, cov, idx, fn, err);
     }
 }
 
@@ -457,16 +452,21 @@ struct pcd_denoiser {
     int32_t* alist = nullptr;
     int32_t* redo = nullptr;
     unsigned* redo_cnt = nullptr;
+    uint8_t* fail = nullptr;      // per active row: anchor test failed
+    void* sel_tmp = nullptr;      // rocprim::select scratch
+    size_t sel_bytes = 0;
     int anchor_ka = 0;            // KA of the stored anchors (0: none)
+    int64_t last_dense = -1;      // rows of the last anchored stage when it re-anchored every row, else -1
     bool anchoring = true;        // anchored kNN for seeded searches (pcd_denoiser_set_anchoring)
     bool loaded = false, iterated = false;
     bool timing = false;
-    std::vector<hipEvent_t> ev;
-    std::vector<float> ms;
+    std::vector<hipEvent_t> ev;   // kTimingSets sets of kTimingEvents events, one set per timed iteration
+    int ev_used = 0;              // sets recorded since set_timing / the last get_timing
     RowMap rowmap() const { return RowMap{rows, rows ? n_rows : n}; }
 };
 
 static const int kNumPart = 1024;
+static const int kTimingSets = 256, kTimingEvents = 8;
 
 static int check_params(const pcd_denoiser* dn, const pcd_denoise_params* p) {
     PCD_CHECK_ARG(dn && p, "null argument");
@@ -491,6 +491,26 @@ static bool phase_is_global(const pcd_denoise_params* p, int ph) {
     return p->phase_kind[ph] == PCD_STEP_FLAT || p->phase_kind[ph] == PCD_STEP_NEW;
 }
 
+// rows whose anchor test failed (fail[t] != 0), in row order -> dn->redo[0 .. *dn->redo_cnt)
+static int select_redo(pcd_denoiser* dn, const RowMap& rm, hipStream_t st) {
+    const size_t n = (size_t)rm.nq;
+    size_t bytes = 0;
+    rocprim::counting_iterator<int32_t> ids(0);
+    if (rm.rows) (void)rocprim::select(nullptr, bytes, rm.rows, dn->fail, dn->redo, dn->redo_cnt, n, st);
+    else (void)rocprim::select(nullptr, bytes, ids, dn->fail, dn->redo, dn->redo_cnt, n, st);
+    if (bytes > dn->sel_bytes) {
+        (void)hipFree(dn->sel_tmp);
+        dn->sel_tmp = nullptr;
+        dn->sel_bytes = 0;
+        if (hipMalloc(&dn->sel_tmp, bytes) != hipSuccess) return fail(PCD_ERR_OOM, "pcd_denoiser: select temp");
+        dn->sel_bytes = bytes;
+    }
+    hipError_t e = rm.rows ? rocprim::select(dn->sel_tmp, bytes, rm.rows, dn->fail, dn->redo, dn->redo_cnt, n, st)
+                           : rocprim::select(dn->sel_tmp, bytes, ids, dn->fail, dn->redo, dn->redo_cnt, n, st);
+    if (e != hipSuccess) return fail(PCD_ERR_HIP, std::string("rocprim::select: ") + hipGetErrorString(e));
+    return PCD_OK;
+}
+
 // Anchored K1 (seeded, list cap K <= 32, KA = 2K): the anchor test for every active row, then a re-anchoring
 // grid search for the rows that failed it -- or for every row when there are no anchors (of this KA) yet.
 static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int K, hipStream_t st) {
@@ -501,35 +521,33 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     if (!dn->anc) {
         if (hipMalloc(&dn->anc, N * sizeof(float4)) != hipSuccess ||
             hipMalloc(&dn->alist, (int64_t)2 * knn_cap(dn->kcap) * N * sizeof(int32_t)) != hipSuccess ||
-            hipMalloc(&dn->redo, N * sizeof(int32_t)) != hipSuccess ||
+            hipMalloc(&dn->redo, N * sizeof(int32_t)) != hipSuccess || hipMalloc(&dn->fail, N) != hipSuccess ||
             hipMalloc(&dn->redo_cnt, sizeof(unsigned)) != hipSuccess)
             return fail(PCD_ERR_OOM, "pcd_denoiser: anchor buffers");
         dn->anchor_ka = 0;
     }
     const bool dense = dn->anchor_ka != KA;
+    dn->last_dense = dense ? rm.nq : -1;
     if (dense) PCD_HIP(hipMemsetAsync(dn->anc, 0xFF, N * sizeof(float4), st));   // NaN radius: no anchor
     const GridView gv = dn->g->view;
     float4* P = dn->pos[dn->cur];
     const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
-    const dim3 grd_redo((unsigned)std::min<int64_t>(cdiv(rm.nq, 256), 2048));
     const dim3 grd_wave((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), dense ? 8192 : 2048));
-    PCD_HIP(hipMemsetAsync(dn->redo_cnt, 0, sizeof(unsigned), st));
+    int rc = PCD_OK;
 #define PCD_K1A(C)                                                                                                     \
     case C:                                                                                                            \
         if (dense) {                                                                                                   \
             hipLaunchKernelGGL((k_knn_redo_wave<2 * C, true>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,    \
                                dn->alist, dn->idx, dn->redo, dn->redo_cnt);                                            \
-            hipLaunchKernelGGL((k_redo_nvt1<C, true>), grd, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore, p->rho,   \
-                               p->tau, p->damp, dn->cov, dn->idx, dn->fn, dn->err, dn->redo, dn->redo_cnt);            \
         } else {                                                                                                       \
-            hipLaunchKernelGGL((k_knn_anchor_nvt1<C, 2 * C>), grd, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore,    \
-                               p->rho, p->tau, p->damp, dn->cov, dn->anc, dn->alist, dn->idx, dn->fn, dn->err,         \
-                               dn->redo, dn->redo_cnt);                                                                \
+            hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd, blk, 0, st, gv, P, N, rm, kstore, dn->anc, dn->alist,    \
+                               dn->idx, dn->fail);                                                                     \
+            if ((rc = select_redo(dn, rm, st)) != PCD_OK) return rc;                                                   \
             hipLaunchKernelGGL((k_knn_redo_wave<2 * C, false>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,   \
                                dn->alist, dn->idx, dn->redo, dn->redo_cnt);                                            \
-            hipLaunchKernelGGL((k_redo_nvt1<C, false>), grd_redo, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore,     \
-                               p->rho, p->tau, p->damp, dn->cov, dn->idx, dn->fn, dn->err, dn->redo, dn->redo_cnt);    \
         }                                                                                                              \
+        hipLaunchKernelGGL((k_nvt1<C>), grd, blk, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore, p->rho, p->tau, \
+                           p->damp, dn->cov, dn->fn, dn->err);                                                         \
         break;
     switch (K) {
         PCD_K1A(8) PCD_K1A(16) PCD_K1A(32)
@@ -689,6 +707,7 @@ int pcd_denoiser_destroy(pcd_denoiser* dn) {
     (void)hipFree(dn->edge); (void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part);
     (void)hipFree(dn->red); (void)hipFree(dn->gscal); (void)hipFree(dn->err);
     (void)hipFree(dn->anc); (void)hipFree(dn->alist); (void)hipFree(dn->redo); (void)hipFree(dn->redo_cnt);
+    (void)hipFree(dn->fail); (void)hipFree(dn->sel_tmp);
     for (auto e : dn->ev) (void)hipEventDestroy(e);
     delete dn;
     return PCD_OK;
@@ -791,6 +810,29 @@ int pcd_denoiser_reset_seed(pcd_denoiser* dn) {
     return PCD_OK;
 }
 
+#ifdef PCD_WKNN_STATS
+int pcd_debug_wstats(unsigned long long* out8, int reset) {
+    PCD_HIP(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_wstats), 8 * sizeof(unsigned long long)));
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        PCD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wstats), z, sizeof z));
+    }
+    return PCD_OK;
+}
+#endif
+
+int pcd_denoiser_anchor_stats(pcd_denoiser* dn, int64_t* redo_rows, void* stream) {
+    PCD_CHECK_ARG(dn && redo_rows, "null argument");
+    *redo_rows = -1;
+    if (!dn->redo_cnt || dn->anchor_ka == 0) return PCD_OK;
+    if (dn->last_dense >= 0) { *redo_rows = dn->last_dense; return PCD_OK; }
+    unsigned c = 0;
+    PCD_HIP(hipMemcpyAsync(&c, dn->redo_cnt, sizeof(unsigned), hipMemcpyDeviceToHost, as_stream(stream)));
+    PCD_HIP(hipStreamSynchronize(as_stream(stream)));
+    *redo_rows = c;
+    return PCD_OK;
+}
+
 int pcd_denoiser_set_anchoring(pcd_denoiser* dn, int enable) {
     PCD_CHECK_ARG(dn != nullptr, "null denoiser");
     dn->anchoring = enable != 0;
@@ -806,8 +848,9 @@ int pcd_denoiser_set_seeding(pcd_denoiser* dn, int enable) {
 int pcd_denoiser_set_timing(pcd_denoiser* dn, int enable) {
     PCD_CHECK_ARG(dn != nullptr, "null denoiser");
     dn->timing = enable != 0;
+    dn->ev_used = 0;
     if (dn->timing && dn->ev.empty()) {
-        dn->ev.resize(8);
+        dn->ev.resize((size_t)kTimingSets * kTimingEvents);
         for (auto& e : dn->ev) PCD_HIP(hipEventCreate(&e));
     }
     return PCD_OK;
@@ -816,15 +859,22 @@ int pcd_denoiser_set_timing(pcd_denoiser* dn, int enable) {
 int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n_written) {
     PCD_CHECK_ARG(dn && ms_out && n_written, "null argument");
     *n_written = 0;
-    if (!dn->timing || dn->ev.empty()) return PCD_OK;
-    PCD_HIP(hipEventSynchronize(dn->ev.back()));
+    if (!dn->timing || dn->ev.empty() || dn->ev_used == 0) return PCD_OK;
+    const int sets = dn->ev_used;
+    PCD_HIP(hipEventSynchronize(dn->ev[(size_t)(sets - 1) * kTimingEvents + kTimingEvents - 1]));
     int w = 0;
-    for (size_t s = 0; s + 1 < dn->ev.size() && w < n_slots; ++s) {
-        float m = 0.f;
-        PCD_HIP(hipEventElapsedTime(&m, dn->ev[s], dn->ev[s + 1]));
-        ms_out[w++] = m;
+    for (int slot = 0; slot + 1 < kTimingEvents && w < n_slots; ++slot) {
+        double acc = 0.0;
+        for (int st = 0; st < sets; ++st) {
+            float m = 0.f;
+            hipEvent_t* e = &dn->ev[(size_t)st * kTimingEvents];
+            PCD_HIP(hipEventElapsedTime(&m, e[slot], e[slot + 1]));
+            acc += m;
+        }
+        ms_out[w++] = (float)(acc / sets);
     }
     *n_written = w;
+    dn->ev_used = 0;
     return PCD_OK;
 }
 
@@ -833,12 +883,13 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
     if (rc != PCD_OK) return rc;
     hipStream_t st = as_stream(stream);
     for (int it = 0; it < iterations; ++it) {
-        const bool rec = dn->timing && it == iterations - 1;
-        if (rec) PCD_HIP(hipEventRecord(dn->ev[0], st));
+        hipEvent_t* ev = nullptr;     // this iteration's event set (timing on, and a set left)
+        if (dn->timing && dn->ev_used < kTimingSets) ev = &dn->ev[(size_t)dn->ev_used++ * kTimingEvents];
+        if (ev) PCD_HIP(hipEventRecord(ev[0], st));
         if ((rc = stage_k1(dn, p, st)) != PCD_OK) return rc;
-        if (rec) PCD_HIP(hipEventRecord(dn->ev[1], st));
+        if (ev) PCD_HIP(hipEventRecord(ev[1], st));
         if ((rc = stage_k2(dn, p, st)) != PCD_OK) return rc;
-        if (rec) PCD_HIP(hipEventRecord(dn->ev[2], st));
+        if (ev) PCD_HIP(hipEventRecord(ev[2], st));
         for (int ph = 0; ph < p->nphases; ++ph) {
             if (phase_is_global(p, ph)) {
                 double* red4 = dn->red + 4 * ph;
@@ -847,13 +898,13 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
                 if ((rc = stage_maxdist(dn, p, ph, nullptr, st)) != PCD_OK) return rc;
             }
             if ((rc = stage_apply(dn, p, ph, nullptr, st)) != PCD_OK) return rc;
-            if (rec) PCD_HIP(hipEventRecord(dn->ev[3 + ph], st));
+            if (ev) PCD_HIP(hipEventRecord(ev[3 + ph], st));
         }
-        if (rec)
-            for (int ph = p->nphases; ph < 3; ++ph) PCD_HIP(hipEventRecord(dn->ev[3 + ph], st));
+        if (ev)
+            for (int ph = p->nphases; ph < 3; ++ph) PCD_HIP(hipEventRecord(ev[3 + ph], st));
         stage_finish(dn);
-        if (rec) PCD_HIP(hipEventRecord(dn->ev[6], st));
-        if (rec) PCD_HIP(hipEventRecord(dn->ev[7], st));
+        if (ev) PCD_HIP(hipEventRecord(ev[6], st));
+        if (ev) PCD_HIP(hipEventRecord(ev[7], st));
     }
     return PCD_OK;
 }

@@ -3,7 +3,8 @@
 // Reference: Selector.__init__ builds scipy KDTree(graph.pos) once and never rebuilds it
 // (Pointcloud/Modules/Selector.py:138-141); getKNNSelection queries the CURRENT positions against that
 // snapshot (Selector.py:235-246).  Here: bbox -> cell size -> Morton keys -> radix sort (rocPRIM) -> sorted
-// float4 snapshot + hash of occupied cells.  Build is one-time and synchronises the stream.
+// float4 snapshot + bricked cell index (hash of occupied 4x4x4 bricks, dense per-brick cell ranges).  Build is
+// one-time and synchronises the stream.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -79,29 +80,39 @@ __global__ void k_gather_sorted(const float* __restrict__ xyz, const int32_t* __
     pts[r] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], __uint_as_float((uint32_t)i));
 }
 
-__global__ void k_count_starts(const unsigned long long* __restrict__ keys, int64_t n, unsigned long long* count) {
+// number of distinct (key >> shift) values of a sorted key array
+__global__ void k_count_starts(const unsigned long long* __restrict__ keys, int64_t n, int shift, unsigned long long* count) {
     const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const bool st = (r < n) && (r == 0 || keys[r] != keys[r - 1]);
+    const bool st = (r < n) && (r == 0 || (keys[r] >> shift) != (keys[r - 1] >> shift));
     const unsigned long long b = __ballot(st);
     if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (unsigned long long)__popcll(b));
 }
 
-__global__ void k_insert(const unsigned long long* __restrict__ keys, int64_t n, HashSlot* table, int hbits,
-                         unsigned long long mask) {
+__global__ void k_brick_flags(const unsigned long long* __restrict__ keys, int64_t n, uint32_t* __restrict__ flag) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r < n) flag[r] = (r == 0 || (keys[r] >> 6) != (keys[r - 1] >> 6)) ? 1u : 0u;
+}
+
+// bidx = inclusive scan of the brick-start flags: row r lies in brick bidx[r] - 1 (bricks numbered in Morton order)
+__global__ void k_insert(const unsigned long long* __restrict__ keys, const uint32_t* __restrict__ bidx, int64_t n,
+                         HashSlot* table, int hbits, unsigned long long mask, uint2* __restrict__ cellr) {
     const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (r >= n) return;
     const unsigned long long key = keys[r];
-    if (r != 0 && keys[r - 1] == key) return;
+    if (r != 0 && keys[r - 1] == key) return;        // one thread per cell
     int64_t end = r + 1;
     while (end < n && keys[end] == key) ++end;
-    unsigned long long slot = hash_slot(key, hbits);
+    const uint32_t b = bidx[r] - 1u;
+    cellr[(uint64_t)b * 64 + (key & 63)] = make_uint2((uint32_t)r, (uint32_t)end);
+    if (r != 0 && (keys[r - 1] >> 6) == (key >> 6)) return;   // one thread per brick inserts it
+    const unsigned long long bkey = key >> 6;
+    unsigned long long slot = hash_slot(bkey, hbits);
     for (;;) {
-        unsigned long long prev = atomicCAS(&table[slot].key, kEmptyKey, key);
-        if (prev == kEmptyKey || prev == key) break;
+        unsigned long long prev = atomicCAS(&table[slot].key, kEmptyKey, bkey);
+        if (prev == kEmptyKey || prev == bkey) break;
         slot = (slot + 1) & mask;
     }
-    table[slot].start = (uint32_t)r;
-    table[slot].end = (uint32_t)end;
+    table[slot].brick = b;
 }
 
 // ------------------------------------------------------------------ query kernels
@@ -289,7 +300,7 @@ int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, const fl
     auto free_tmp = [&]() { (void)hipFree(keys); (void)hipFree(keys2); (void)hipFree(vals); (void)hipFree(tmp); (void)hipFree(cnt); };
     if (hipMalloc(&keys, n * 8) != hipSuccess || hipMalloc(&keys2, n * 8) != hipSuccess ||
         hipMalloc(&vals, n * 4) != hipSuccess || hipMalloc(&g->perm, n * 4) != hipSuccess ||
-        hipMalloc(&g->pts, n * sizeof(float4)) != hipSuccess || hipMalloc(&cnt, 8) != hipSuccess) {
+        hipMalloc(&g->pts, n * sizeof(float4)) != hipSuccess || hipMalloc(&cnt, 16) != hipSuccess) {
         free_tmp(); cleanup(); return fail(PCD_ERR_OOM, "pcd_grid_build: device allocation");
     }
     const dim3 blk(256), grd((unsigned)cdiv(n, 256));
@@ -300,24 +311,45 @@ int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, const fl
         free_tmp(); cleanup(); return fail(PCD_ERR_HIP, "rocprim::radix_sort_pairs failed");
     }
     hipLaunchKernelGGL(k_gather_sorted, grd, blk, 0, st, xyz, g->perm, n, g->pts);
-    (void)hipMemsetAsync(cnt, 0, 8, st);
-    hipLaunchKernelGGL(k_count_starts, grd, blk, 0, st, keys2, n, cnt);
-    unsigned long long cells = 0;
-    (void)hipMemcpyAsync(&cells, cnt, 8, hipMemcpyDeviceToHost, st);
+    (void)hipMemsetAsync(cnt, 0, 16, st);
+    hipLaunchKernelGGL(k_count_starts, grd, blk, 0, st, keys2, n, 0, cnt);
+    hipLaunchKernelGGL(k_count_starts, grd, blk, 0, st, keys2, n, 6, cnt + 1);
+    unsigned long long counts[2] = {0, 0};
+    (void)hipMemcpyAsync(counts, cnt, 16, hipMemcpyDeviceToHost, st);
     e = hipStreamSynchronize(st);
     if (e != hipSuccess) { free_tmp(); cleanup(); return fail(PCD_ERR_HIP, std::string("grid sort: ") + hipGetErrorString(e)); }
-    g->cells = (int64_t)cells;
+    g->cells = (int64_t)counts[0];
+    g->bricks = (int64_t)counts[1];
     int hbits = 1;
-    while ((1ll << hbits) < 4 * (int64_t)cells) ++hbits;
+    while ((1ll << hbits) < 2 * g->bricks) ++hbits;
     g->slots = 1ll << hbits;
-    if (hipMalloc(&g->table, g->slots * sizeof(HashSlot)) != hipSuccess) { free_tmp(); cleanup(); return fail(PCD_ERR_OOM, "hash table"); }
+    uint32_t* bflag = reinterpret_cast<uint32_t*>(vals);   // vals is free after the sort: reuse for the flags,
+    uint32_t* bidx = reinterpret_cast<uint32_t*>(keys);    // keys (pre-sort) for their scan
+    if (hipMalloc(&g->table, g->slots * sizeof(HashSlot)) != hipSuccess ||
+        hipMalloc(&g->cellr, g->bricks * 64 * sizeof(uint2)) != hipSuccess) {
+        free_tmp(); cleanup(); return fail(PCD_ERR_OOM, "brick table");
+    }
     (void)hipMemsetAsync(g->table, 0xFF, g->slots * sizeof(HashSlot), st);
-    hipLaunchKernelGGL(k_insert, grd, blk, 0, st, keys2, n, g->table, hbits, (unsigned long long)(g->slots - 1));
+    (void)hipMemsetAsync(g->cellr, 0, g->bricks * 64 * sizeof(uint2), st);
+    hipLaunchKernelGGL(k_brick_flags, grd, blk, 0, st, keys2, n, bflag);
+    size_t scan_bytes = 0;
+    (void)rocprim::inclusive_scan(nullptr, scan_bytes, bflag, bidx, (size_t)n, rocprim::plus<uint32_t>(), st);
+    if (scan_bytes > tmp_bytes) {
+        (void)hipFree(tmp);
+        tmp = nullptr;
+        if (hipMalloc(&tmp, scan_bytes) != hipSuccess) { free_tmp(); cleanup(); return fail(PCD_ERR_OOM, "scan temp"); }
+    }
+    if (rocprim::inclusive_scan(tmp, scan_bytes, bflag, bidx, (size_t)n, rocprim::plus<uint32_t>(), st) != hipSuccess) {
+        free_tmp(); cleanup(); return fail(PCD_ERR_HIP, "rocprim::inclusive_scan failed");
+    }
+    hipLaunchKernelGGL(k_insert, grd, blk, 0, st, keys2, bidx, n, g->table, hbits, (unsigned long long)(g->slots - 1),
+                       g->cellr);
     e = hipStreamSynchronize(st);
     free_tmp();
     if (e != hipSuccess) { cleanup(); return fail(PCD_ERR_HIP, std::string("grid hash: ") + hipGetErrorString(e)); }
     v.pts = g->pts;
     v.table = g->table;
+    v.cells = g->cellr;
     v.hbits = hbits;
     v.mask = (unsigned long long)(g->slots - 1);
     *out = g;
@@ -329,6 +361,7 @@ int pcd_grid_destroy(pcd_grid* g) {
     (void)hipFree(g->pts);
     (void)hipFree(g->perm);
     (void)hipFree(g->table);
+    (void)hipFree(g->cellr);
     delete g;
     return PCD_OK;
 }

@@ -139,8 +139,180 @@ PCD_DEV void rot_cols(float Z[3][3], int j, float ct, float st) {
     }
 }
 
-// ssteqr(compz='I') for n = 3: d[3] diagonal, e[2] off-diagonal -> eigenvalues (ascending) in d, vectors in Z
+// ssteqr(compz='I') for n = 3: d[3] diagonal, e[2] off-diagonal -> eigenvalues (ascending) in d, vectors in Z.
+// LAPACK's loop specialised to n = 3 so that every array index is a compile-time constant: the only blocks are
+// [0,1] / [1,2] (one slaev2 or a deflation) and [0,2] (implicit QL or QR sweeps over both rotations, then a
+// 2x2 tail).  Same operations in the same order as the general loop (ssteqr3_generic), so the results are
+// bit-identical (tools/eigh_equiv.cpp); on the GPU it avoids the select chains of runtime-indexed registers.
+PCD_DEV void rot_cols_c(float Z[3][3], int j, float ct, float st) {   // rot_cols, branch-free (j constant)
+    const bool id = (ct == 1.f && st == 0.f);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float t = Z[i][j + 1], z = Z[i][j];
+        const float n1 = ct * t - st * z, n0 = st * t + ct * z;
+        Z[i][j + 1] = id ? t : n1;
+        Z[i][j] = id ? z : n0;
+    }
+}
+// QL deflation test of e[m] between d[m], d[m+1]; QR test of e[m] between d[m+1], d[m]
+PCD_DEV bool ql_small(float e, float dm, float dm1) {
+    return fabsf(e) * fabsf(e) <= (kEps * kEps * fabsf(dm)) * fabsf(dm1) + kSafmin;
+}
+// slaev2 on rows/cols (J, J+1) -> Z columns J, J+1
+template <int J>
+PCD_DEV void tail2(float d[3], float e[2], float Z[3][3]) {
+    float rt1, rt2, c, s;
+    slaev2(d[J], e[J], d[J + 1], rt1, rt2, c, s);
+    rot_cols_c(Z, J, c, s);
+    d[J] = rt1; d[J + 1] = rt2; e[J] = 0.f;
+}
+PCD_DEV void ql_sweep3(float d[3], float e[2], float Z[3][3]) {   // l = 0, m = 2
+    float p = d[0];
+    float g = (d[1] - p) / (2.f * e[0]);
+    float r = slapy2(g, 1.f);
+    g = d[2] - p + (e[0] / (g + fsign(r, g)));
+    float s = 1.f, c = 1.f;
+    p = 0.f;
+    float f = s * e[1], b = c * e[1];
+    slartg(g, f, c, s, r);
+    g = d[2] - p;
+    r = (d[1] - g) * s + 2.f * c * b;
+    p = s * r;
+    d[2] = g + p;
+    g = c * r - b;
+    const float c1 = c, s1 = -s;
+    f = s * e[0]; b = c * e[0];
+    slartg(g, f, c, s, r);
+    e[1] = r;
+    g = d[1] - p;
+    r = (d[0] - g) * s + 2.f * c * b;
+    p = s * r;
+    d[1] = g + p;
+    g = c * r - b;
+    rot_cols_c(Z, 1, c1, s1);
+    rot_cols_c(Z, 0, c, -s);
+    d[0] = d[0] - p;
+    e[0] = g;
+}
+PCD_DEV void qr_sweep3(float d[3], float e[2], float Z[3][3]) {   // l = 2, m = 0
+    float p = d[2];
+    float g = (d[1] - p) / (2.f * e[1]);
+    float r = slapy2(g, 1.f);
+    g = d[0] - p + (e[1] / (g + fsign(r, g)));
+    float s = 1.f, c = 1.f;
+    p = 0.f;
+    float f = s * e[0], b = c * e[0];
+    slartg(g, f, c, s, r);
+    g = d[0] - p;
+    r = (d[1] - g) * s + 2.f * c * b;
+    p = s * r;
+    d[0] = g + p;
+    g = c * r - b;
+    const float c0 = c, s0 = s;
+    f = s * e[1]; b = c * e[1];
+    slartg(g, f, c, s, r);
+    e[0] = r;
+    g = d[1] - p;
+    r = (d[2] - g) * s + 2.f * c * b;
+    p = s * r;
+    d[1] = g + p;
+    g = c * r - b;
+    rot_cols_c(Z, 0, c0, s0);
+    rot_cols_c(Z, 1, c, s);
+    d[2] = d[2] - p;
+    e[1] = g;
+}
+// a 2x2 block [J, J+1] in the outer loop: deflate or slaev2 (direction only changes the deflation test's order)
+template <int J>
+PCD_DEV void block2(float d[3], float e[2], float Z[3][3]) {
+    const float anorm = fmaxf(fmaxf(fmaxf(0.f, fabsf(d[J])), fabsf(d[J + 1])), fabsf(e[J]));   // NaNs drop out, as in LAPACK's loop
+    if (anorm == 0.f) return;
+    const bool qr = fabsf(d[J + 1]) < fabsf(d[J]);
+    const bool small = qr ? ql_small(e[J], d[J + 1], d[J]) : ql_small(e[J], d[J], d[J + 1]);
+    if (small) e[J] = 0.f;
+    else tail2<J>(d, e, Z);
+}
 PCD_DEV void ssteqr3(float d[3], float e[2], float Z[3][3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Z[i][j] = (i == j) ? 1.f : 0.f;
+    const int nmaxit = 3 * 30;
+    auto split = [&](int mm) {
+        const float tst = fabsf(e[mm]);
+        if (tst == 0.f) return true;
+        if (tst <= (sqrtf(fabsf(d[mm])) * sqrtf(fabsf(d[mm + 1]))) * kEps) { e[mm] = 0.f; return true; }
+        return false;
+    };
+    if (split(0)) {                       // blocks [0,0] [1,...]
+        e[0] = 0.f;
+        if (split(1)) e[1] = 0.f;         // [1,1] [2,2]
+        else block2<1>(d, e, Z);          // [1,2]
+    } else if (split(1)) {                // [0,1] [2,2]
+        block2<0>(d, e, Z);
+        e[1] = 0.f;
+    } else {                              // [0,2]
+        float anorm = fmaxf(fmaxf(fmaxf(0.f, fabsf(d[0])), fabsf(d[1])), fabsf(d[2]));
+        anorm = fmaxf(fmaxf(anorm, fabsf(e[0])), fabsf(e[1]));
+        if (anorm != 0.f) {
+            int jtot = 0;
+            if (!(fabsf(d[2]) < fabsf(d[0]))) {
+                // QL from the top: l = 0 until e[0] or e[1] deflates, then the 2x2 tail [1,2] or [0,1]
+                int l = 0;
+                for (;;) {
+                    if (l == 0) {
+                        if (ql_small(e[0], d[0], d[1])) { e[0] = 0.f; l = 1; continue; }
+                        if (ql_small(e[1], d[1], d[2])) { e[1] = 0.f; tail2<0>(d, e, Z); break; }
+                        if (jtot == nmaxit) break;
+                        ++jtot;
+                        ql_sweep3(d, e, Z);
+                    } else {                  // l == 1: block [1,2]
+                        if (ql_small(e[1], d[1], d[2])) e[1] = 0.f;
+                        else tail2<1>(d, e, Z);
+                        break;
+                    }
+                }
+            } else {
+                // QR from the bottom: l = 2 until e[1] or e[0] deflates, then the tail [0,1] or [1,2]
+                int l = 2;
+                for (;;) {
+                    if (l == 2) {
+                        if (ql_small(e[1], d[2], d[1])) { e[1] = 0.f; l = 1; continue; }
+                        if (ql_small(e[0], d[1], d[0])) { e[0] = 0.f; tail2<1>(d, e, Z); break; }
+                        if (jtot == nmaxit) break;
+                        ++jtot;
+                        qr_sweep3(d, e, Z);
+                    } else {                  // l == 1: block [0,1]
+                        if (ql_small(e[0], d[1], d[0])) e[0] = 0.f;
+                        else tail2<0>(d, e, Z);
+                        break;
+                    }
+                }
+            }
+        }
+    }
+    // selection sort, ascending (swaps columns of Z)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        int k = i;
+        float p = d[i];
+#pragma unroll
+        for (int j = i + 1; j < 3; ++j)
+            if (d[j] < p) { k = j; p = d[j]; }
+#pragma unroll
+        for (int kk = i + 1; kk < 3; ++kk) {
+            if (k == kk) {
+                d[kk] = d[i]; d[i] = p;
+#pragma unroll
+                for (int r = 0; r < 3; ++r) { const float t = Z[r][i]; Z[r][i] = Z[r][kk]; Z[r][kk] = t; }
+            }
+        }
+    }
+}
+#ifdef PCD_EIGH_GENERIC
+// ssteqr(compz='I') for n = 3 written as LAPACK's general loop (runtime block indices).  Kept only as the
+// reference for tools/eigh_equiv.cpp, which checks ssteqr3 below against it bit for bit.
+PCD_DEV void ssteqr3_generic(float d[3], float e[2], float Z[3][3]) {
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -281,8 +453,10 @@ PCD_DEV void ssteqr3(float d[3], float e[2], float Z[3][3]) {
         }
     }
 }
+#endif
 }  // namespace lapack
 
+template <int IMPL = 0>   // IMPL 1 (tools/eigh_equiv.cpp only): LAPACK's general ssteqr loop
 PCD_DEV void eigh3(Sym3 A, float w[3], float V[3][3]) {
     using namespace lapack;
     float a22 = A.a11, a32 = A.a12, a33 = A.a22;
@@ -309,6 +483,9 @@ PCD_DEV void eigh3(Sym3 A, float w[3], float V[3][3]) {
     float d[3] = {A.a00, a22, a33};
     float e[2] = {e1, a32};
     float Z[3][3];
+#ifdef PCD_EIGH_GENERIC
+    if (IMPL == 1) ssteqr3_generic(d, e, Z); else
+#endif
     ssteqr3(d, e, Z);
     // sormtr: Z := H(1) Z on rows 2..3
     if (tau != 0.f) {

@@ -28,16 +28,17 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // One 16-byte hash slot: Morton key of an occupied cell -> [start, end) in the sorted snapshot.
-struct HashSlot {
+struct HashSlot {            // one occupied BRICK (4x4x4 cells): Morton brick key -> brick index
     unsigned long long key;
-    uint32_t start, end;
+    uint32_t brick, pad;
 };
 static constexpr unsigned long long kEmptyKey = ~0ull;
 
 // Kernel-side view of a grid (passed by value).
 struct GridView {
     const float4* pts;       // snapshot, Morton-sorted, w unused
-    const HashSlot* table;
+    const HashSlot* table;   // occupied bricks (open addressing, load <= 1/2)
+    const uint2* cells;      // [bricks][64] (start, end) snapshot rows of each cell; start == end: empty
     unsigned long long mask; // table slots - 1
     int hbits;               // log2(slots)
     float ox, oy, oz, h, inv_h;
@@ -54,6 +55,8 @@ struct pcd_grid {
     float4* pts = nullptr;     // [n]
     int32_t* perm = nullptr;   // [n] sorted rank -> original index
     pcd::HashSlot* table = nullptr;
+    uint2* cellr = nullptr;    // [bricks][64]
     int64_t slots = 0;
+    int64_t bricks = 0;
     pcd::GridView view{};
 };

@@ -1,7 +1,7 @@
 // Exact k-nearest-neighbour search over the frozen snapshot (replaces scipy KDTree.query on the snapshot
 // taken in Selector.__init__, Pointcloud/Modules/Selector.py:141,243).
 //
-// Index: Morton-sorted snapshot points + an open-addressed hash of occupied cells (GridView).  A query scans
+// Index: Morton-sorted snapshot points + a bricked cell index (GridView, cell_range).  A query scans
 // its cell and the 26 around it (centre, faces, edges, corners), pruning any cell whose box is farther than
 // the current k-th distance, then expands Chebyshev shells until the k-th distance is provably below the
 // distance to every unscanned cell.  The top-k lives in registers as a sorted list of 64-bit keys
@@ -28,15 +28,22 @@ __host__ __device__ inline unsigned long long hash_slot(unsigned long long key, 
     return (key * 0x9E3779B97F4A7C15ull) >> (64 - hbits);
 }
 
+// Cells live in bricks of 4x4x4: the brick is found in a small hash of occupied bricks (L2-resident), the cell's
+// row range in the brick's dense 64-entry block (contiguous in memory, and nearby bricks are nearby in Morton order),
+// so the probes of neighbouring queries share cache lines instead of each touching a random hash slot.
 PCD_DEV bool cell_range(const GridView& g, int cx, int cy, int cz, uint32_t& s, uint32_t& e) {
     if ((unsigned)cx >= (unsigned)g.dx || (unsigned)cy >= (unsigned)g.dy || (unsigned)cz >= (unsigned)g.dz)
         return false;
-    const unsigned long long key = morton3(cx, cy, cz);
-    unsigned long long slot = hash_slot(key, g.hbits);
+    const unsigned long long key = morton3(cx, cy, cz), bkey = key >> 6;
+    unsigned long long slot = hash_slot(bkey, g.hbits);
     for (;;) {
         const uint4 sl = *reinterpret_cast<const uint4*>(g.table + slot);
         const unsigned long long k2 = (unsigned long long)sl.x | ((unsigned long long)sl.y << 32);
-        if (k2 == key) { s = sl.z; e = sl.w; return true; }
+        if (k2 == bkey) {
+            const uint2 c = g.cells[(uint64_t)sl.z * 64 + (key & 63)];
+            s = c.x; e = c.y;
+            return c.y > c.x;
+        }
         if (k2 == kEmptyKey) return false;
         slot = (slot + 1) & g.mask;
     }

@@ -11,11 +11,18 @@ namespace pcd {
 // T_i  = Σ w n_j n_jᵀ / Σ w,  all w := 1 when Σ w = 0                 (Decompositionor.py:291-299)
 // UNROLL > 0: the neighbour loop is fully unrolled to UNROLL (>= cnt) so register-resident neighbour lists stay
 // in registers and every gather of the list can be issued before the first is consumed.
+//
+// The binary vote is decided on a fast estimate of c (hardware sqrt / reciprocal instead of the IEEE sqrt, three
+// divisions and acos) whenever the estimate is farther from the threshold cos(rho) than its error bound; only the
+// rare pairs within that margin (or with a degenerate |dv|²) evaluate the reference expression exactly.  Since
+// acos is monotone, the vote is the same either way: the estimate's error is ~1e-6 (|dn| <= 1, 1-ulp hardware
+// ops), the margin 4e-6·(1 + |n_j|₁), and cos(rho) vs acos's own rounding differ by < 1e-6.
 template <int UNROLL = 0, class P, class Nr, class Nb>
 PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho) {
     float w00 = 0.f, w01 = 0.f, w02 = 0.f, w11 = 0.f, w12 = 0.f, w22 = 0.f;
     float u00 = 0.f, u01 = 0.f, u02 = 0.f, u11 = 0.f, u12 = 0.f, u22 = 0.f;
     int wsum = 0;
+    const float cthr = cosf(rho);
     auto body = [&](int t) {
         const int64_t j = nb(t);
         const Vec3 vj = pos(j), nj = nrm(j);
@@ -23,15 +30,23 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho) {
 #if defined(PCD_EXP_NOVOTE)
         const bool w = dv.x > 0.f;
 #else
-        const float den = fmaxf(sqrtf(sq3(dv)), 1e-12f);
-        const Vec3 dn = v3(dv.x / den, dv.y / den, dv.z / den);
-        float c = dot3(dn, nj);
-        c = fabsf(fminf(fmaxf(c, -1.f), 1.f));
-#if defined(PCD_EXP_NOACOS)
-        const bool w = c < rho;
+        const float sq = sq3(dv);
+#ifdef __HIP_DEVICE_COMPILE__
+        const float inv = __builtin_amdgcn_rcpf(fmaxf(__builtin_amdgcn_sqrtf(sq), 1e-12f));
 #else
-        const bool w = acosf(c) > rho;
+        const float inv = 1.f / fmaxf(sqrtf(sq), 1e-12f);
 #endif
+        float ca = (dv.x * inv * nj.x + dv.y * inv * nj.y) + dv.z * inv * nj.z;
+        ca = fabsf(fminf(fmaxf(ca, -1.f), 1.f));
+        const float marg = 4e-6f * (1.f + fabsf(nj.x) + fabsf(nj.y) + fabsf(nj.z));
+        bool w = ca < cthr;
+        if (!(fabsf(ca - cthr) > marg) || !(sq > 1e-30f && sq < 1e30f)) {   // near the threshold: exact
+            const float den = fmaxf(sqrtf(sq), 1e-12f);
+            const Vec3 dn = v3(dv.x / den, dv.y / den, dv.z / den);
+            float c = dot3(dn, nj);
+            c = fabsf(fminf(fmaxf(c, -1.f), 1.f));
+            w = acosf(c) > rho;
+        }
 #endif
         const float o00 = nj.x * nj.x, o01 = nj.x * nj.y, o02 = nj.x * nj.z;
         const float o11 = nj.y * nj.y, o12 = nj.y * nj.z, o22 = nj.z * nj.z;

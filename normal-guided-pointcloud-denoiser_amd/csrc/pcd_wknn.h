@@ -4,10 +4,11 @@
 // VGPRs and every accepted candidate runs a 64-step select chain, so a sparse set of queries (the 1-3 % that fail
 // the anchor test) runs at 2 waves/SIMD on long serial chains.  Here the 64 lanes split one query's work instead:
 //   1. the cells of the box [q - r, q + r] (r = sqrt of the acceptance cap) are dealt one per lane, pruned by
-//      box distance, probed in the hash table in parallel, and their point counts wave-scanned;
-//   2. the flattened candidate rows are dealt one per lane per pass (cell found by a binary search of the scan in
-//      LDS); a key (d² bits << 32 | rank) below the cap is appended to the wave's LDS survivor buffer with one
-//      ballot-compaction per pass;
+//      box distance and probed in the hash table in parallel;
+//   2. the chunk's candidate rows are flattened (count scan in LDS, binary-searched per row) and dealt kWaveRows
+//      per lane per round, all
+//      loads of a round in flight together; a key (d² bits << 32 | rank) below the cap is appended to the wave's
+//      LDS survivor buffer with one ballot compaction per row slot;
 //   3. the survivors (a few more than K when the cap is tight) are bitonic-sorted across the wave in registers
 //      (4 keys per lane, slot-major: key e lives in lane e % 64, slot e / 64), so lane t ends with the t-th key.
 // A full buffer is reduced in place (sort, keep the K best, tighten the cap), so any cap >= the true K-th key is
@@ -19,6 +20,12 @@
 namespace pcd {
 
 static constexpr int kWaveSurv = 256;   // survivor slots per wave (4 per lane)
+#ifdef PCD_WKNN_STATS   // experiment builds only: queries, chunks, candidate rows, reduces, final survivors, sorts>128
+__device__ unsigned long long g_wstats[8];
+#define PCD_WSTAT(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_wstats[i], (unsigned long long)(v)); } while (0)
+#else
+#define PCD_WSTAT(i, v) ((void)0)
+#endif
 
 PCD_DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -74,6 +81,7 @@ PCD_DEV void wave_bitonic_sort(unsigned long long (&v)[M], int lane) {
 // Sort the cnt (<= kWaveSurv) survivors of buf; on return lane t's `top` is the t-th smallest key (kInfKey pad).
 // If keep > 0, the keep smallest are written back to buf[0..keep) and the count returned.
 PCD_DEV unsigned long long wave_sort_survivors(unsigned long long* buf, int cnt, int lane, int keep, int& kept) {
+    wave_sync();                             // every lane's appends are visible
     unsigned long long top;
     if (cnt <= 64) {
         unsigned long long v[1] = {lane < cnt ? buf[lane] : kInfKey};
@@ -105,21 +113,41 @@ PCD_DEV unsigned long long wave_sort_survivors(unsigned long long* buf, int cnt,
 
 struct WaveCells {          // per-wave LDS scratch for one chunk of <= 64 cells
     uint32_t start[64];
-    uint32_t end_excl[64];  // inclusive scan of the counts (flattened candidate end of each cell)
+    uint32_t end_incl[64];  // inclusive scan of the counts: flattened candidate end of each cell
 };
 
+// Append the keys < cap of one candidate row per lane to the wave's survivor buffer (one ballot compaction).
+PCD_DEV void wave_append(bool pass, unsigned long long key, unsigned long long* buf, int& cnt, int lane) {
+    const unsigned long long m = __ballot(pass);
+    if (pass) buf[cnt + __popcll(m & ((1ull << lane) - 1ull))] = key;
+    cnt += __popcll(m);
+}
+
 // Scan the cells of box [lo, hi] (cell coords), appending keys < cap to buf.  cap may tighten (buffer reduce).
+// Latency-shaped: one round of hash probes per chunk of 64 cells, then the chunk's flattened candidate rows in
+// rounds of kWaveRows per lane -- every row index first (binary search of the count scan in LDS), then all the
+// point loads at once, then the keys -- so a query costs a handful of dependent memory round trips.
+static constexpr int kWaveRows = 8;
 template <int K>
 PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int hi[3], unsigned long long& cap,
                            unsigned long long* buf, int& cnt, WaveCells* wc, int lane) {
+    // box extents in cells: the caller's r keeps them far below 2^10 per axis except for a pathological query,
+    // whose box is clamped to the grid; 64-bit only for the (rare) giant product
     const int ex = hi[0] - lo[0] + 1, ey = hi[1] - lo[1] + 1, ez = hi[2] - lo[2] + 1;
     const int64_t nc = (int64_t)ex * ey * ez;
+    const bool small = nc < (1ll << 31);
+    const uint32_t exy = (uint32_t)ex * (uint32_t)ey;
     for (int64_t base = 0; base < nc; base += 64) {
-        // 1. one cell per lane: prune by box distance, probe, count
         uint32_t s = 0, e = 0;
         const int64_t ci = base + lane;
         if (ci < nc) {
-            const int cx = lo[0] + (int)(ci % ex), cy = lo[1] + (int)((ci / ex) % ey), cz = lo[2] + (int)(ci / ((int64_t)ex * ey));
+            int cx, cy, cz;
+            if (small) {
+                const uint32_t c32 = (uint32_t)ci, zq = c32 / exy, rem = c32 - zq * exy, yq = rem / (uint32_t)ex;
+                cx = lo[0] + (int)(rem - yq * (uint32_t)ex); cy = lo[1] + (int)yq; cz = lo[2] + (int)zq;
+            } else {
+                cx = lo[0] + (int)(ci % ex); cy = lo[1] + (int)((ci / ex) % ey); cz = lo[2] + (int)(ci / ((int64_t)ex * ey));
+            }
             const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
             const float gx = axis_gap(q.x, lx, lx + g.h), gy = axis_gap(q.y, ly, ly + g.h), gz = axis_gap(q.z, lz, lz + g.h);
             const float kth = __uint_as_float((unsigned)(cap >> 32));
@@ -134,35 +162,48 @@ PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int
             if (lane >= o) incl += t;
         }
         const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+        PCD_WSTAT(1, 1);
+        PCD_WSTAT(2, total);
         if (total == 0) continue;
+        wave_sync();                         // the previous chunk's readers are done with wc
         wc->start[lane] = s;
-        wc->end_excl[lane] = incl;
+        wc->end_incl[lane] = incl;
         wave_sync();
-        // 2. flattened candidates, one per lane per pass
-        for (uint32_t j0 = 0; j0 < total; j0 += 64) {
-            if (cnt > kWaveSurv - 64) {      // make room: keep the K best, tighten the cap
-                int kept;
-                const unsigned long long top = wave_sort_survivors(buf, cnt, lane, K, kept);
-                const unsigned long long kth_key = __shfl(top, K - 1);
-                if (kept == K && kth_key + 1ull < cap) cap = kth_key + 1ull;
-                cnt = kept;
-            }
-            const uint32_t j = j0 + lane;
-            bool pass = false;
-            unsigned long long key = 0;
-            if (j < total) {
-                int a = 0, b = 63;           // first cell with end_excl > j
-                while (a < b) {
+        for (uint32_t j0 = 0; j0 < total; j0 += 64 * kWaveRows) {
+            uint32_t r[kWaveRows];
+#pragma unroll
+            for (int u = 0; u < kWaveRows; ++u) {
+                const uint32_t j = j0 + (uint32_t)(u * 64 + lane);
+                r[u] = 0u;
+                if (j0 + (uint32_t)(u * 64) >= total) continue;   // wave-uniform: slot past the chunk
+                int a = 0, b = 63;           // first cell whose inclusive end exceeds j
+#pragma unroll
+                for (int it = 0; it < 6; ++it) {
                     const int m = (a + b) >> 1;
-                    if (wc->end_excl[m] > j) b = m; else a = m + 1;
+                    if (wc->end_incl[m] > j) b = m; else a = m + 1;
                 }
-                const uint32_t r = wc->start[a] + (j - (a ? wc->end_excl[a - 1] : 0u));
-                key = cand_key<false>(q, g.pts[r], r);
-                pass = key < cap;
+                r[u] = j < total ? wc->start[a] + (j - (a ? wc->end_incl[a - 1] : 0u)) : 0u;
             }
-            const unsigned long long m = __ballot(pass);
-            if (pass) buf[cnt + __popcll(m & ((1ull << lane) - 1ull))] = key;
-            cnt += __popcll(m);
+            float4 p[kWaveRows];
+#pragma unroll
+            for (int u = 0; u < kWaveRows; ++u)
+                if (j0 + (uint32_t)(u * 64) < total) p[u] = g.pts[r[u]];
+#pragma unroll
+            for (int u = 0; u < kWaveRows; ++u) {
+                const uint32_t j = j0 + (uint32_t)(u * 64 + lane);
+                if (j0 + (uint32_t)(u * 64) < total) {
+                    if (cnt > kWaveSurv - 64) {  // make room: keep the K best, tighten the cap
+                        PCD_WSTAT(3, 1);
+                        int kept;
+                        const unsigned long long top = wave_sort_survivors(buf, cnt, lane, K, kept);
+                        const unsigned long long kth_key = __shfl(top, K - 1);
+                        if (kept == K && kth_key + 1ull < cap) cap = kth_key + 1ull;
+                        cnt = kept;
+                    }
+                    const unsigned long long key = cand_key<false>(q, p[u], r[u]);
+                    wave_append(j < total && key < cap, key, buf, cnt, lane);
+                }
+            }
             wave_sync();
         }
     }
@@ -216,6 +257,10 @@ PCD_DEV unsigned long long wave_knn(const GridView& g, Vec3 q, unsigned long lon
     const float r = sqrtf(__uint_as_float((unsigned)(cap >> 32))) * 1.0001f + 1e-30f;
     cell_box(g, q, r, lo, hi);
     wave_scan_box<K>(g, q, lo, hi, cap, buf, cnt, wc, lane);
+    PCD_WSTAT(0, 1);
+    PCD_WSTAT(4, cnt);
+    PCD_WSTAT(5, cnt > 128);
+    PCD_WSTAT(6, (hi[0] - lo[0] + 1) * (hi[1] - lo[1] + 1) * (hi[2] - lo[2] + 1));
     int kept;
     return wave_sort_survivors(buf, cnt, lane, 0, kept);
 }

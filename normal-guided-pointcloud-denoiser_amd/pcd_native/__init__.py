@@ -70,6 +70,7 @@ _SIGS = {
     "pcd_denoiser_reset_seed": (c_int, [c_void_p]),
     "pcd_denoiser_set_seeding": (c_int, [c_void_p, c_int]),
     "pcd_denoiser_set_anchoring": (c_int, [c_void_p, c_int]),
+    "pcd_denoiser_anchor_stats": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_denoiser_check": (c_int, [c_void_p, c_void_p]),
     "pcd_denoiser_set_rows": (c_int, [c_void_p, c_void_p, c_int64]),
     "pcd_denoiser_set_coverage": (c_int, [c_void_p, c_void_p, c_void_p]),
@@ -249,6 +250,13 @@ class FusedDenoiser:
 
     def set_anchoring(self, enable=True):
         check(lib().pcd_denoiser_set_anchoring(self.handle, int(bool(enable))), "pcd_denoiser_set_anchoring")
+
+    def redo_rows(self) -> int:
+        """Rows re-anchored by the last anchored kNN stage (-1: none ran)."""
+        v = ctypes.c_int64(0)
+        check(lib().pcd_denoiser_anchor_stats(self.handle, ctypes.byref(v), c_void_p(stream_ptr())),
+              "pcd_denoiser_anchor_stats")
+        return v.value
 
     def reset_seed(self):
         check(lib().pcd_denoiser_reset_seed(self.handle), "pcd_denoiser_reset_seed")

@@ -41,34 +41,36 @@ def main():
     params = nat.make_params(k=k, k_update=8, d=d)
     grid = proc.selector.grid
     print(f"n={n} d=2l={d:.4g}", flush=True)
-    anchors = {}
-    for kp in (40, 48, 64):
-        idx, d2 = grid.knn(snap, kp, with_d2=True)
-        anchors[kp] = [snap.clone(), idx, d2[:, -1].sqrt()]
+    # (K', lambda): anchor lists of K' points; a failing query is re-anchored at q + lambda * (q - q_prev)
+    variants = [(64, 0.0), (64, -0.5), (64, -0.25), (64, -1.0)]
+    idx0 = {}
+    for kp in sorted({v[0] for v in variants}):
+        idx0[kp] = grid.knn(snap, kp, with_d2=True)
+    anchors = {v: [snap.clone(), idx0[v[0]][0].clone(), idx0[v[0]][1][:, -1].sqrt()] for v in variants}
     prev = snap.clone()
     cur = torch.empty_like(snap)
     for it in range(1, iters + 1):
         fused.iterate(params, 1)
         fused.store(cur)
-        _, d2k = grid.knn(prev, k, with_d2=True)     # d_k at the position this iteration's kNN used
-        dk = d2k[:, -1].sqrt()
         mv = (cur - prev).norm(dim=1)
-        line = f"it {it}: move/d_k {q(mv / dk)}  moved>0 {float((mv > 0).float().mean()):.3f}"
-        # certification at the NEXT query position (cur)
-        for kp, (a, S, D) in anchors.items():
+        line = f"it {it}: moved>0 {float((mv > 0).float().mean()):.3f}"
+        for (kp, lam), (a, S, D) in anchors.items():
             delta = (cur - a).norm(dim=1)
-            dS = (snap[S] - cur[:, None, :]).norm(dim=2)          # [n, kp]
-            kth = dS.kthvalue(k, dim=1).values
-            ok = kth < (D - delta) * (1 - 1e-5)
-            fail = ~ok
-            line += f" | K'={kp} fail {float(fail.float().mean()):.4f}"
+            fail = torch.zeros(n, dtype=torch.bool, device=dev)
+            for c0 in range(0, n, 2_000_000):                     # chunks: [n, kp] distance blocks
+                sl = slice(c0, min(n, c0 + 2_000_000))
+                dS = (snap[S[sl]] - cur[sl, None, :]).norm(dim=2)
+                kth = dS.kthvalue(k, dim=1).values
+                fail[sl] = ~(kth < (D[sl] - delta[sl]) * (1 - 1e-5))
+                del dS
+            line += f" | K'={kp} lam={lam:g} fail {float(fail.float().mean()) * 100:5.2f}%"
             if fail.any():
                 fi = fail.nonzero().squeeze(1)
-                i2, dd2 = grid.knn(cur[fi], kp, with_d2=True)
-                a[fi] = cur[fi]
+                at = cur[fi] + lam * (cur[fi] - prev[fi])
+                i2, dd2 = grid.knn(at, kp, with_d2=True)
+                a[fi] = at
                 S[fi] = i2
                 D[fi] = dd2[:, -1].sqrt()
-            del dS
         print(line, flush=True)
         prev.copy_(cur)
 
