@@ -111,13 +111,9 @@ PCD_DEV void k1_epilogue(const float4* __restrict__ pos, const float4* __restric
 #else
     const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho);
     const float4 n4 = nrm[i];
-#ifdef PCD_EXP_NOEIGH
-    const Vec3 f = v3(T.a00 + n4.x, T.a01 + T.a11, T.a02 + T.a22 + T.a12);
-#else
     float w[3], V[3][3];
     eigh3(T, w, V);
     const Vec3 f = vu_smooth(w, V, v3(n4.x, n4.y, n4.z), tau, damp);
-#endif
     __builtin_nontemporal_store(v4f{f.x, f.y, f.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
 #endif
 }
@@ -320,17 +316,30 @@ __global__ __launch_bounds__(256) void k_nvt2(const float4* __restrict__ pos, co
 
 struct RedC { double sx, sy, sz, cnt; };
 
+// The k_u neighbour rows of point i, all loads in flight together (KU = compile-time bound on ku).
+template <int KU>
+PCD_DEV void gather_rows(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N, int64_t i, int ku,
+                         float4 (&v)[KU]) {
+    int32_t j[KU];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) j[u] = idx[(int64_t)(u < ku ? u : ku - 1) * N + i];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) v[u] = pos[j[u]];
+}
+
 // Flat-phase centre, pass 1: per-block f64 partial sums of the k_u neighbour rows of the class-c points.
+template <int KU>
 __global__ void k_class_rows_sum(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N, RowMap rm,
                                  int ku, const uint8_t* __restrict__ cls, int c, RedC* __restrict__ part) {
     double sx = 0, sy = 0, sz = 0, cnt = 0;
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < rm.nq; t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = rm(t);
         if (cls[i] != c) continue;
-        for (int u = 0; u < ku; ++u) {
-            const float4 v = pos[idx[(int64_t)u * N + i]];
-            sx += v.x; sy += v.y; sz += v.z;
-        }
+        float4 v[KU];
+        gather_rows<KU>(pos, idx, N, i, ku, v);
+#pragma unroll
+        for (int u = 0; u < KU; ++u)
+            if (u < ku) { sx += v[u].x; sy += v[u].y; sz += v[u].z; }
         cnt += ku;
     }
     __shared__ double s[4][256];
@@ -371,6 +380,7 @@ __global__ void k_centre(const double* __restrict__ red, float* __restrict__ g) 
 }
 
 // pass 4: delta = max ||v_j - centre|| over the same rows (Denoiser.py:107), atomicMax on the f32 bits.
+template <int KU>
 __global__ void k_class_rows_maxdist(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N,
                                      RowMap rm, int ku, const uint8_t* __restrict__ cls, int c, float* __restrict__ g) {
     const Vec3 ctr = v3(g[0], g[1], g[2]);
@@ -378,10 +388,11 @@ __global__ void k_class_rows_maxdist(const float4* __restrict__ pos, const int32
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < rm.nq; t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = rm(t);
         if (cls[i] != c) continue;
-        for (int u = 0; u < ku; ++u) {
-            const float4 v = pos[idx[(int64_t)u * N + i]];
-            mx = fmaxf(mx, sqrtf(sq3(v3(v.x, v.y, v.z) - ctr)));
-        }
+        float4 v[KU];
+        gather_rows<KU>(pos, idx, N, i, ku, v);
+#pragma unroll
+        for (int u = 0; u < KU; ++u)
+            if (u < ku) mx = fmaxf(mx, sqrtf(sq3(v3(v[u].x, v[u].y, v[u].z) - ctr)));
     }
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
     if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(g) + 3, __float_as_uint(mx));
@@ -392,7 +403,7 @@ __global__ void k_copy_delta(const float* __restrict__ from, float* __restrict__
 }
 
 // K3: one Gauss-Seidel phase: active points of class c move (reading pin), other active points copy through.
-template <int KIND>
+template <int KIND, int KU>
 __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, float4* __restrict__ pout,
                                                 const float4* __restrict__ fn, const float4* __restrict__ edge,
                                                 const int32_t* __restrict__ idx, int64_t N, RowMap rm, int ku,
@@ -407,11 +418,11 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     const Rows4 P{pin}, F{fn};
     const ColNb nb{idx, N, i};
     Vec3 o;
-    if (KIND == PCD_STEP_FLAT) o = step_flat(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
-    else if (KIND == PCD_STEP_EDGE) o = step_edge(P, F, vi, Rows4{edge}(i), ku, nb, d, alpha);
-    else if (KIND == PCD_STEP_FEATURE) o = step_feature<false>(P, F, vi, F(i), ku, nb, 1.f, d, alpha);
-    else if (KIND == PCD_STEP_NEW) o = step_feature<true>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
-    else if (KIND == PCD_STEP_CORNER) o = step_corner(P, F, vi, ku, nb, d, alpha);
+    if (KIND == PCD_STEP_FLAT) o = step_flat<KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
+    else if (KIND == PCD_STEP_EDGE) o = step_edge<KU>(P, F, vi, Rows4{edge}(i), ku, nb, d, alpha);
+    else if (KIND == PCD_STEP_FEATURE) o = step_feature<false, KU>(P, F, vi, F(i), ku, nb, 1.f, d, alpha);
+    else if (KIND == PCD_STEP_NEW) o = step_feature<true, KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
+    else if (KIND == PCD_STEP_CORNER) o = step_corner<KU>(P, F, vi, ku, nb, d, alpha);
     else o = vi;
     store4(pout, i, o);
 }
@@ -606,8 +617,15 @@ static int stage_k2(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t s
 // local (Σx, Σy, Σz, count) of phase ph -> red4 (device)
 static int stage_sum(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, double* red4, hipStream_t st) {
     const int c = p->phase_class[ph];
-    hipLaunchKernelGGL(k_class_rows_sum, dim3(kNumPart), dim3(256), 0, st, dn->pos[dn->cur], dn->idx, dn->n,
-                       dn->rowmap(), p->k_update, dn->cls, c, dn->part);
+#define PCD_RS(C) hipLaunchKernelGGL(k_class_rows_sum<C>, dim3(kNumPart), dim3(256), 0, st, dn->pos[dn->cur], dn->idx, \
+                                     dn->n, dn->rowmap(), p->k_update, dn->cls, c, dn->part)
+    switch (knn_cap(p->k_update)) {
+        case 8: PCD_RS(8); break;
+        case 16: PCD_RS(16); break;
+        case 32: PCD_RS(32); break;
+        default: PCD_RS(64); break;
+    }
+#undef PCD_RS
     hipLaunchKernelGGL(k_part_reduce, dim3(1), dim3(256), 0, st, dn->part, kNumPart, red4);
     PCD_LAUNCH_CHECK();
     return PCD_OK;
@@ -622,8 +640,15 @@ static int stage_centre(pcd_denoiser* dn, int ph, const double* red4, hipStream_
 // local max distance of phase ph -> gscal delta (and *red1 when given)
 static int stage_maxdist(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, float* red1, hipStream_t st) {
     float* gs = dn->gscal + 4 * ph;
-    hipLaunchKernelGGL(k_class_rows_maxdist, dim3(kNumPart), dim3(256), 0, st, dn->pos[dn->cur], dn->idx, dn->n,
-                       dn->rowmap(), p->k_update, dn->cls, p->phase_class[ph], gs);
+#define PCD_MD(C) hipLaunchKernelGGL(k_class_rows_maxdist<C>, dim3(kNumPart), dim3(256), 0, st, dn->pos[dn->cur], \
+                                     dn->idx, dn->n, dn->rowmap(), p->k_update, dn->cls, p->phase_class[ph], gs)
+    switch (knn_cap(p->k_update)) {
+        case 8: PCD_MD(8); break;
+        case 16: PCD_MD(16); break;
+        case 32: PCD_MD(32); break;
+        default: PCD_MD(64); break;
+    }
+#undef PCD_MD
     if (red1) hipLaunchKernelGGL(k_copy_delta, dim3(1), dim3(64), 0, st, gs + 3, red1);
     PCD_LAUNCH_CHECK();
     return PCD_OK;
@@ -639,7 +664,14 @@ static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, co
     float4* pout = dn->pos[dn->cur ^ 1];
     if (rm.nq > 0) {
         const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
-#define PCD_PH(KD) hipLaunchKernelGGL(k_phase<KD>, grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, dn->n, rm, p->k_update, dn->cls, c, gs, p->d, a)
+#define PCD_PH2(KD, C) hipLaunchKernelGGL((k_phase<KD, C>), grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, dn->n, rm, p->k_update, dn->cls, c, gs, p->d, a)
+#define PCD_PH(KD)                                                                                                     \
+    switch (knn_cap(p->k_update)) {                                                                                    \
+        case 8: PCD_PH2(KD, 8); break;                                                                                 \
+        case 16: PCD_PH2(KD, 16); break;                                                                               \
+        case 32: PCD_PH2(KD, 32); break;                                                                               \
+        default: PCD_PH2(KD, 64); break;                                                                               \
+    }
         switch (kind) {
             case PCD_STEP_FLAT: PCD_PH(PCD_STEP_FLAT); break;
             case PCD_STEP_EDGE: PCD_PH(PCD_STEP_EDGE); break;
@@ -649,6 +681,7 @@ static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, co
             default: PCD_PH(PCD_STEP_DUMMY); break;
         }
 #undef PCD_PH
+#undef PCD_PH2
         PCD_LAUNCH_CHECK();
     }
     dn->cur ^= 1;

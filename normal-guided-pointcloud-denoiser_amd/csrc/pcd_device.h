@@ -458,6 +458,11 @@ PCD_DEV void ssteqr3_generic(float d[3], float e[2], float Z[3][3]) {
 
 template <int IMPL = 0>   // IMPL 1 (tools/eigh_equiv.cpp only): LAPACK's general ssteqr loop
 PCD_DEV void eigh3(Sym3 A, float w[3], float V[3][3]) {
+#ifdef PCD_EXP_NOEIGH     // experiment builds only: timing without the eigen-solver (results wrong)
+    w[0] = A.a00; w[1] = A.a11; w[2] = A.a22;
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) V[r][c] = r == c ? A.a01 : A.a12;
+    return;
+#endif
     using namespace lapack;
     float a22 = A.a11, a32 = A.a12, a33 = A.a22;
     const float a21 = A.a01, a31 = A.a02;

@@ -6,6 +6,35 @@
 
 namespace pcd {
 
+static constexpr int kNbBatch = 8;   // neighbours gathered together (every load of a batch in flight)
+
+// Neighbour loop of a fused kernel: M = compile-time bound on cnt (list cap).  The list entries are read first, then
+// the neighbours' (v_j, n_j) in batches of kNbBatch whose loads are all issued before any is consumed; f(vj, nj) runs
+// for t < cnt in list order, so every sum keeps the reference's summation order.  M = 0: plain runtime loop.
+template <int M, class P, class Nr, class Nb, class F>
+PCD_DEV void for_neighbours(P pos, Nr nrm, int cnt, Nb nb, F&& f) {
+    if constexpr (M > 0) {
+        int32_t jj[M];
+#pragma unroll
+        for (int t = 0; t < M; ++t) jj[t] = (int32_t)nb(t < cnt ? t : cnt - 1);
+#pragma unroll
+        for (int b = 0; b < M; b += kNbBatch) {
+            constexpr int B = M < kNbBatch ? M : kNbBatch;
+            Vec3 vb[B], nv[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u) { vb[u] = pos(jj[b + u]); nv[u] = nrm(jj[b + u]); }
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (b + u < cnt) f(vb[u], nv[u]);
+        }
+    } else {
+        for (int t = 0; t < cnt; ++t) {
+            const int64_t j = nb(t);
+            f(pos(j), nrm(j));
+        }
+    }
+}
+
 // ----------------------------------------------------------------- H5: Decompositionor.getBetterFilteredNVT
 // w_ij = acos(|clamp(normalize(v_j - v_i) . n_j, -1, 1)|) > rho       (Decompositionor.py:290; F.normalize eps 1e-12)
 // T_i  = Σ w n_j n_jᵀ / Σ w,  all w := 1 when Σ w = 0                 (Decompositionor.py:291-299)
@@ -23,9 +52,7 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho) {
     float u00 = 0.f, u01 = 0.f, u02 = 0.f, u11 = 0.f, u12 = 0.f, u22 = 0.f;
     int wsum = 0;
     const float cthr = cosf(rho);
-    auto body = [&](int t) {
-        const int64_t j = nb(t);
-        const Vec3 vj = pos(j), nj = nrm(j);
+    auto body2 = [&](const Vec3 vj, const Vec3 nj) {
         const Vec3 dv = vj - vi;
 #if defined(PCD_EXP_NOVOTE)
         const bool w = dv.x > 0.f;
@@ -53,13 +80,7 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho) {
         u00 += o00; u01 += o01; u02 += o02; u11 += o11; u12 += o12; u22 += o22;
         if (w) { w00 += o00; w01 += o01; w02 += o02; w11 += o11; w12 += o12; w22 += o22; ++wsum; }
     };
-    if constexpr (UNROLL > 0) {
-#pragma unroll
-        for (int t = 0; t < UNROLL; ++t)
-            if (t < cnt) body(t);
-    } else {
-        for (int t = 0; t < cnt; ++t) body(t);
-    }
+    for_neighbours<UNROLL>(pos, nrm, cnt, nb, body2);
     Sym3 T;
     if (wsum == 0) {
         const float c = (float)cnt;
@@ -110,13 +131,11 @@ PCD_DEV Vec3 clamp_step(Vec3 vi, Vec3 x, float alpha, float d) {
 
 // ----------------------------------------------------------------- H9: Denoiser.flat_step (Denoiser.py:90-119)
 // delta is the GLOBAL max ||v_j - centre|| over every row of the selection (computed by the caller).
-template <class P, class Nr, class Nb>
+template <int M = 0, class P, class Nr, class Nb>
 PCD_DEV Vec3 step_flat(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float delta, float d, float alpha) {
     const float dd = delta * delta;
     float sx = 0.f, sy = 0.f, sz = 0.f, ws = 0.f;
-    for (int t = 0; t < cnt; ++t) {
-        const int64_t j = nb(t);
-        const Vec3 vj = pos(j), nj = nrm(j);
+    for_neighbours<M>(pos, nrm, cnt, nb, [&](const Vec3 vj, const Vec3 nj) {
         const Vec3 dist = vj - vi;
         const float sim = expf((-16.f * sq3(ni - nj)) / dd);
         const float clo = expf((-4.f * sq3(dist)) / dd);
@@ -124,22 +143,20 @@ PCD_DEV Vec3 step_flat(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float de
         const float wd = W * dot3(nj, dist);
         sx += wd * ni.x; sy += wd * ni.y; sz += wd * ni.z;
         ws += W;
-    }
+    });
     const Vec3 di = v3(sx / ws * alpha, sy / ws * alpha, sz / ws * alpha);
     const float nrm2 = sqrtf(sq3(di));
     return (nrm2 <= d) ? vi + di : vi;   // NaN (Σ W = 0) -> no move, as di[~mask] = 0
 }
 
 // ----------------------------------------------------------------- H10: Denoiser.edge_step (Denoiser.py:53-88)
-template <class P, class Nr, class Nb>
+template <int M = 0, class P, class Nr, class Nb>
 PCD_DEV Vec3 step_edge(P pos, Nr nrm, Vec3 vi, Vec3 y, int cnt, Nb nb, float d, float alpha) {
     float A[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
     Vec3 b = v3(0.f, 0.f, 0.f);
     const Vec3 yyvi = outer_mul(y, vi);
     const float yc[3] = {y.x, y.y, y.z};
-    for (int t = 0; t < cnt; ++t) {
-        const int64_t j = nb(t);
-        const Vec3 vj = pos(j), nj = nrm(j);
+    for_neighbours<M>(pos, nrm, cnt, nb, [&](const Vec3 vj, const Vec3 nj) {
         const Vec3 vjp = vj - dot3(vj - vi, y) * y;
         const Vec3 njp = nj - dot3(nj, y) * y;
         const float nc[3] = {njp.x, njp.y, njp.z};
@@ -148,7 +165,7 @@ PCD_DEV Vec3 step_edge(P pos, Nr nrm, Vec3 vi, Vec3 y, int cnt, Nb nb, float d, 
 #pragma unroll
             for (int q = 0; q < 3; ++q) A[r][q] += nc[r] * nc[q] + yc[r] * yc[q];
         b = b + (outer_mul(njp, vjp) + yyvi);
-    }
+    });
     Vec3 x;
     if (!solve3(A, b, x)) x = vi;
     return clamp_step(vi, x, alpha, d);
@@ -156,15 +173,13 @@ PCD_DEV Vec3 step_edge(P pos, Nr nrm, Vec3 vi, Vec3 y, int cnt, Nb nb, float d, 
 
 // ----------------------------------------------------------------- H11: Denoiser.feature_step (Denoiser.py:174-219)
 //                                 and H12: Denoiser.new_step (Denoiser.py:121-172; WEIGHTED=true)
-template <bool WEIGHTED, class P, class Nr, class Nb>
+template <bool WEIGHTED, int M = 0, class P, class Nr, class Nb>
 PCD_DEV Vec3 step_feature(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float delta, float d, float alpha) {
     float S[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};  // Σ w nj njᵀ
     Vec3 svj = v3(0.f, 0.f, 0.f);                                       // Σ w vj
     Vec3 snv = v3(0.f, 0.f, 0.f);                                       // Σ w (nj njᵀ) vj
     const float dd = delta * delta;
-    for (int t = 0; t < cnt; ++t) {
-        const int64_t j = nb(t);
-        const Vec3 vj = pos(j), nj = nrm(j);
+    for_neighbours<M>(pos, nrm, cnt, nb, [&](const Vec3 vj, const Vec3 nj) {
         float w = 1.f;
         if (WEIGHTED) {
             const float dt = dot3(nj, vj - vi);
@@ -178,7 +193,7 @@ PCD_DEV Vec3 step_feature(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float
         svj = svj + (WEIGHTED ? w * vj : vj);
         const Vec3 nv = outer_mul(nj, vj);
         snv = snv + (WEIGHTED ? w * nv : nv);
-    }
+    });
     const float nc[3] = {ni.x, ni.y, ni.z};
     const float card = (float)cnt;
     float A[3][3];
@@ -196,16 +211,14 @@ PCD_DEV Vec3 step_feature(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float
 }
 
 // ----------------------------------------------------------------- H12: Denoiser.corner_step (Denoiser.py:26-51)
-template <class P, class Nr, class Nb>
+template <int M = 0, class P, class Nr, class Nb>
 PCD_DEV Vec3 step_corner(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float d, float alpha) {
     float A[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
     Vec3 b = v3(0.f, 0.f, 0.f);
-    for (int t = 0; t < cnt; ++t) {
-        const int64_t j = nb(t);
-        const Vec3 vj = pos(j), nj = nrm(j);
+    for_neighbours<M>(pos, nrm, cnt, nb, [&](const Vec3 vj, const Vec3 nj) {
         add_outer(A, nj);
         b = b + outer_mul(nj, vj);
-    }
+    });
     Vec3 x;
     if (!solve3(A, b, x)) x = vi;
     return clamp_step(vi, x, alpha, d);
