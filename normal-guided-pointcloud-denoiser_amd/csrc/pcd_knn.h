@@ -285,7 +285,7 @@ PCD_DEV void topk_merge(TopK<K>& tk, unsigned long long (&c)[B]) {
 // buf = this lane's column of the block's [M][kCapStride] u32 row buffer.
 static constexpr int kCapStride = 256;
 
-template <int K, int M>
+template <int K, int M, int S = kCapStride>
 PCD_DEV void cap_drain(const GridView& g, Vec3 q, TopK<K>& tk, const uint32_t* buf, int cnt) {
     // unrolled over the (bounded) chunk count: the list stays in place, no loop-carried copy of it
 #pragma unroll
@@ -295,7 +295,7 @@ PCD_DEV void cap_drain(const GridView& g, Vec3 q, TopK<K>& tk, const uint32_t* b
 #pragma unroll
             for (int b = 0; b < 8; ++b) {
                 const bool ok = base + b < cnt;
-                const uint32_t r = ok ? buf[(base + b) * kCapStride] : 0u;
+                const uint32_t r = ok ? buf[(base + b) * S] : 0u;
                 const float4 p = g.pts[r];
                 c[b] = ok ? cand_key<false>(q, p, r) : kInfKey;
             }
@@ -305,7 +305,7 @@ PCD_DEV void cap_drain(const GridView& g, Vec3 q, TopK<K>& tk, const uint32_t* b
     }
 }
 
-template <int K, int M>
+template <int K, int M, int S = kCapStride>   // S: row stride of the block's LDS buffer (= threads per block)
 struct CapState {
     unsigned long long lim;  // acceptance cap: every key < lim is buffered
     int cnt;                 // rows in the buffer
@@ -316,27 +316,27 @@ struct CapState {
     PCD_DEV float kth() const { return __uint_as_float((unsigned)(lim >> 32)); }
 };
 
-template <int K, int M>
-PCD_DEV void cap_overflow(const GridView& g, Vec3 q, CapState<K, M>& st) {
+template <int K, int M, int S>
+PCD_DEV void cap_overflow(const GridView& g, Vec3 q, CapState<K, M, S>& st) {
     static_assert(M >= K + 8, "the buffer must hold the K best rows plus room to grow");
     TopK<K> t;
     t.init(st.lim);
-    cap_drain<K, M>(g, q, t, st.buf, st.cnt);
+    cap_drain<K, M, S>(g, q, t, st.buf, st.cnt);
     int n = 0;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        if (t.key[j] != kInfKey) { st.buf[n * kCapStride] = (uint32_t)(t.key[j] & 0xFFFFFFFFull); ++n; }
+        if (t.key[j] != kInfKey) { st.buf[n * S] = (uint32_t)(t.key[j] & 0xFFFFFFFFull); ++n; }
     }
     st.cnt = n;
     if (n == K) st.lim = t.key[K - 1] + 1ull;
 }
 
-template <int K, int M>
-PCD_DEV void cap_scan(const GridView& g, Vec3 q, CapState<K, M>& st, uint32_t s, uint32_t e) {
+template <int K, int M, int S>
+PCD_DEV void cap_scan(const GridView& g, Vec3 q, CapState<K, M, S>& st, uint32_t s, uint32_t e) {
     // groups of 4 rows: 4 loads in flight per lane; the buffer keeps 4 rows of slack for the group's appends
 #pragma unroll 1
     for (uint32_t r = s; r < e; r += 4) {
-        if (st.cnt > M - 4) cap_overflow<K, M>(g, q, st);
+        if (st.cnt > M - 4) cap_overflow<K, M, S>(g, q, st);
         float4 p[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) p[u] = g.pts[min(r + u, e - 1)];
@@ -344,30 +344,30 @@ PCD_DEV void cap_scan(const GridView& g, Vec3 q, CapState<K, M>& st, uint32_t s,
         for (int u = 0; u < 4; ++u) {
             const unsigned long long c = cand_key<false>(q, p[u], r + u);
             if (r + u < e && c < st.lim) {
-                st.buf[st.cnt * kCapStride] = r + u;
+                st.buf[st.cnt * S] = r + u;
                 ++st.cnt;
             }
         }
     }
 }
 
-template <int K, int M>
-PCD_DEV void cap_visit(const GridView& g, Vec3 q, int cx, int cy, int cz, CapState<K, M>& st) {
+template <int K, int M, int S>
+PCD_DEV void cap_visit(const GridView& g, Vec3 q, int cx, int cy, int cz, CapState<K, M, S>& st) {
     const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
     const float gx = axis_gap(q.x, lx, lx + g.h), gy = axis_gap(q.y, ly, ly + g.h), gz = axis_gap(q.z, lz, lz + g.h);
     if (gx * gx + gy * gy + gz * gz > st.kth() * 1.00001f + 1e-30f) return;
     uint32_t s, e;
-    if (cell_range(g, cx, cy, cz, s, e)) cap_scan<K, M>(g, q, st, s, e);
+    if (cell_range(g, cx, cy, cz, s, e)) cap_scan<K, M, S>(g, q, st, s, e);
 }
 
-template <int K, int M>
+template <int K, int M, int S = kCapStride>
 PCD_DEV void knn_search_capped(const GridView& g, Vec3 q, TopK<K>& tk, unsigned long long cap, uint32_t* buf) {
-    CapState<K, M> st{cap, 0, buf};
+    CapState<K, M, S> st{cap, 0, buf};
     const int cx = min(max(cell_coord(q.x, g.ox, g.inv_h), 0), g.dx - 1);
     const int cy = min(max(cell_coord(q.y, g.oy, g.inv_h), 0), g.dy - 1);
     const int cz = min(max(cell_coord(q.z, g.oz, g.inv_h), 0), g.dz - 1);
 #pragma unroll 1
-    for (int t = 0; t < 27; ++t) cap_visit<K, M>(g, q, cx + kRing1[t][0], cy + kRing1[t][1], cz + kRing1[t][2], st);
+    for (int t = 0; t < 27; ++t) cap_visit<K, M, S>(g, q, cx + kRing1[t][0], cy + kRing1[t][1], cz + kRing1[t][2], st);
     int R = 1;
 #pragma unroll 1
     while (!search_done(g, q, cx, cy, cz, R, st.kth())) {
@@ -375,7 +375,7 @@ PCD_DEV void knn_search_capped(const GridView& g, Vec3 q, TopK<K>& tk, unsigned 
         if (R > 24) {  // pathological outlier: exhaustive scan from an empty buffer
             st.cnt = 0;
             st.lim = cap;
-            cap_scan<K, M>(g, q, st, 0, (uint32_t)g.n);
+            cap_scan<K, M, S>(g, q, st, 0, (uint32_t)g.n);
             break;
         }
 #pragma unroll 1
@@ -385,12 +385,12 @@ PCD_DEV void knn_search_capped(const GridView& g, Vec3 q, TopK<K>& tk, unsigned 
                 const bool rim = (dz == -R || dz == R || dy == -R || dy == R);
                 const int step = rim ? 1 : 2 * R;
 #pragma unroll 1
-                for (int dx = -R; dx <= R; dx += step) cap_visit<K, M>(g, q, cx + dx, cy + dy, cz + dz, st);
+                for (int dx = -R; dx <= R; dx += step) cap_visit<K, M, S>(g, q, cx + dx, cy + dy, cz + dz, st);
             }
         }
     }
     tk.init(st.lim);
-    cap_drain<K, M>(g, q, tk, buf, st.cnt);
+    cap_drain<K, M, S>(g, q, tk, buf, st.cnt);
 #ifdef PCD_KNN_STATS
     tk.stat[3] += st.cnt;  // rows left in the buffer at the end
 #endif
