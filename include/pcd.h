@@ -12,7 +12,10 @@
  *   pcd_knn                         Selector.getKNNSelection                   Pointcloud/Modules/Selector.py:235-246
  *                                   torch_cluster.knn_graph (loop=False)       Pointcloud/Modules/GraphBuilder.py:60-63
  *                                   torch_geometric.nn.pool.knn (k=1)          Pointcloud/Modules/Utils.py:253-295
+ *   pcd_radius_count / _fill        Selector.getPointsInRangeSelection(Vectorized)  Pointcloud/Modules/Selector.py:214-233
  *   pcd_nvt_csr                     Decompositionor.getBetterFilteredNVT       Pointcloud/Modules/Decompositionor.py:278-300
+ *   pcd_nvt_normal_csr              Decompositionor.getNormalFilteredNVT       Pointcloud/Modules/Decompositionor.py:260-276
+ *   pcd_pvt_normal_csr              Decompositionor.getNormalFilteredPVT       Pointcloud/Modules/Decompositionor.py:172-211
  *   pcd_vu_smooth                   Decomposition.getVUSmoothedNormals         Pointcloud/Modules/Decompositionor.py:92-106
  *   pcd_classify                    Decomposition.getNVTFeatures/getClasses    Pointcloud/Modules/Decompositionor.py:57-69
  *   pcd_pca_dense                   GraphBuilder.getPVTDecompositionWithKNN    Pointcloud/Modules/GraphBuilder.py:99-111
@@ -82,6 +85,15 @@ int pcd_grid_perm(const pcd_grid* g, int32_t* perm, void* stream);
 int pcd_knn(const pcd_grid* g, const float* q, int64_t nq, int k, void* idx_out, int idx_bits, int sorted_ids,
             int exclude_self, float* d2_out, void* stream);
 
+/* Radius selection over the frozen snapshot (scipy query_ball_point semantics: float64 ((dx²+dy²)+dz²) <= r²,
+ * members in ascending ORIGINAL index).  Two calls: count [nq] (int64), then, with the caller's exclusive prefix
+ * sums offsets [nq+1] and total = offsets[nq], fill idx_out [total] (int64).  fill synchronises `stream`.
+ * radii: fp32 [nq] per query (the reference builds a torch.float radius tensor, Selector.py:233). */
+int pcd_radius_count(const pcd_grid* g, const float* q, int64_t nq, const float* radii, int64_t* counts,
+                     void* stream);
+int pcd_radius_fill(const pcd_grid* g, const float* q, int64_t nq, const float* radii, const int64_t* offsets,
+                    int64_t total, int64_t* idx_out, void* stream);
+
 /* Diagnostic: total work of a kNN(k) pass over q (spatial-order ids), summed over queries into out6 (device u64):
  * cells considered, cells probed in the hash, cells found, candidates scanned, sorted inserts (variant 0:
  * per-candidate insertion) or batch merges (variant 1: batched search, k > 8), extra rings. */
@@ -92,6 +104,14 @@ int pcd_knn_stats(const pcd_grid* g, const float* q, int64_t nq, int k, int vari
 /* CSR selection: segment r has centre ci[r] and neighbours nbr[off[r] .. off[r+1]); all int64 (torch long). */
 int pcd_nvt_csr(const float* pos, const float* n, int64_t npts, const int64_t* ci, const int64_t* off,
                 const int64_t* nbr, int64_t m, float rho, float* eigval, float* eigvec, void* stream);
+/* Normal-filtered NVT (CPSD): w_ij = acos(clamp(n_i . n_j)) <= rho; T_i = sum w n_j n_j^T / sum w, or n_i n_i^T when
+ * no neighbour votes.  Same CSR and outputs as pcd_nvt_csr. */
+int pcd_nvt_normal_csr(const float* n, int64_t npts, const int64_t* ci, const int64_t* off, const int64_t* nbr,
+                       int64_t m, float rho, float* eigval, float* eigvec, void* stream);
+/* Normal-filtered PVT (CPSD): same vote; every w := 1 when none votes; weighted covariance of v_j about their
+ * weighted mean / sum w; an empty neighbourhood gets the reference's cross-product samples.  Outputs as above. */
+int pcd_pvt_normal_csr(const float* pos, const float* n, int64_t npts, const int64_t* ci, const int64_t* off,
+                       const int64_t* nbr, int64_t m, float rho, float* eigval, float* eigvec, void* stream);
 /* eigval [m][3] ascending, eigvec [m][3][3] (columns), n [m][3] -> f_n [m][3] */
 int pcd_vu_smooth(const float* eigval, const float* eigvec, const float* n, int64_t m, float tau, float damp,
                   float* out, void* stream);

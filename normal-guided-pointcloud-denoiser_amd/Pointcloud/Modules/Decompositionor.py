@@ -3,6 +3,8 @@
 getBetterFilteredNVT -> pcd_nvt_csr: per segment, gather (v_j, n_j), threshold, accumulate the 6 unique entries of
 T, Σw = 0 fallback, in-register 3x3 Jacobi eigen-decomposition (reference Decompositionor.py:278-300).
 Decomposition.getVUSmoothedNormals -> pcd_vu_smooth (:92-106); getNVTFeatures / getClasses -> pcd_classify (:57-69).
+CPSD path: getNormalFilteredNVT -> pcd_nvt_normal_csr (:260-276), getNormalFilteredPVT -> pcd_pvt_normal_csr
+(:172-211), Decomposition.getVUFeatures (:84-85).
 """
 from __future__ import annotations
 
@@ -42,6 +44,7 @@ class Decomposition:
         return cls.to(self.eigval.device)
 
     def getVUFeatures(self, tau: float) -> torch.Tensor:
+        """Decompositionor.py:84-85: number of eigenvalues below tau, mod 3."""
         return (self.eigval < tau).sum(dim=1) % 3
 
     def getVUSmoothedNormals(self, n: torch.Tensor, tau: float = 0.3, d: float = 3):
@@ -61,4 +64,18 @@ class Decompositionor:
         pos = _nat.f32(self.graph.pos)
         ev, evec = _nat.nvt_csr(pos, _nat.f32(_n), _nat.i64(selection.i), _nat.i64(selection.slices),
                                 _nat.i64(selection.j), rho)
+        return Decomposition(ev.to(dev), evec.to(dev))
+
+    def getNormalFilteredNVT(self, selection: Selection, _n: torch.Tensor, rho: float = 0.9) -> Decomposition:
+        """w_ij = acos(n_i . n_j) <= rho; T_i = Σ w n_j n_jᵀ / Σ w, n_i n_iᵀ where nothing votes."""
+        dev = self.graph.pos.device
+        ev, evec = _nat.nvt_normal_csr(_nat.f32(_n), _nat.i64(selection.i), _nat.i64(selection.slices),
+                                       _nat.i64(selection.j), rho)
+        return Decomposition(ev.to(dev), evec.to(dev))
+
+    def getNormalFilteredPVT(self, selection: Selection, _n: torch.Tensor, rho: float = 0.9) -> Decomposition:
+        """Weighted covariance of the voting neighbours about their weighted mean (all vote if none does)."""
+        dev = self.graph.pos.device
+        ev, evec = _nat.pvt_normal_csr(_nat.f32(self.graph.pos), _nat.f32(_n), _nat.i64(selection.i),
+                                       _nat.i64(selection.slices), _nat.i64(selection.j), rho)
         return Decomposition(ev.to(dev), evec.to(dev))

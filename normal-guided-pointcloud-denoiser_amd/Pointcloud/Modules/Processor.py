@@ -48,6 +48,27 @@ class Processor:
         decomposition = self.decompositionor.getBetterFilteredNVT(selection, filtered_normals, angle)
         return decomposition, filtered_normals
 
+    # ------------------------------------------------------------------ CPSD ("Martin") feature path
+    def getMartinFeatureDecomposition(self, r: float, rho: float = 0.9):
+        """Processor.py:102-108: radius selection -> normal-filtered NVT -> VU smoothing -> normal-filtered PVT."""
+        _n = self.graph.n
+        selection = self.selector.getPointsInRangeSelection(r)
+        nvt = self.decompositionor.getNormalFilteredNVT(selection, _n, rho)
+        filtered_normals = nvt.getVUSmoothedNormals(_n)
+        decomposition = self.decompositionor.getNormalFilteredPVT(selection, filtered_normals, rho)
+        return decomposition, filtered_normals
+
+    def getVUDecomposition(self):
+        """Processor.py:83-100: r = 2 x the mean kNN(6) graph edge length, rho = 0.95 for both votes."""
+        _graph = self.graph
+        _graph.edge_index = self.graphBuilder.getKNNEdgeIndex(6)
+        mean_graph_edge_length = TorchUtils.averageEdgeLength(_graph.pos, _graph.edge_index)
+        r = 2 * mean_graph_edge_length
+        selection = self.selector.getPointsInRangeSelection(float(r))
+        decompositionNVT = self.decompositionor.getNormalFilteredNVT(selection, _graph.n, rho=0.95)
+        filtered_normals = decompositionNVT.getVUSmoothedNormals(_graph.n, tau=0.3, d=3)
+        return self.decompositionor.getNormalFilteredPVT(selection, filtered_normals, rho=0.95)
+
     # ------------------------------------------------------------------ fused loop
     def _fused_for(self, k_max: int) -> _nat.FusedDenoiser:
         if self._fused is None or self._fused.k_max < k_max:

@@ -130,6 +130,26 @@ class Selector:
         # frozen snapshot of the positions at construction (never rebuilt), like scipy KDTree(graph.pos)
         self.grid = _nat.Grid(graph.pos, k_hint=k_hint)
 
+    def getPointsInRangeSelectionVectorized(self, radii: torch.Tensor, indices: torch.Tensor = None) -> Selection:
+        """Selector.py:214-230: every frozen-snapshot point within radii[r] of the r-th query (current position of
+        indices[r], or of point r), ascending index -- scipy query_ball_point, here pcd_radius_count/_fill."""
+        TorchUtils.validateIndices(indices)
+        _graph = self.graph
+        N = _graph.num_nodes if indices is None else indices.size(0)
+        device = radii.device
+        assert radii.dim() == 1
+        assert radii.size(0) == N, f"Actual: {radii.size(0)}\nExpected: {N}"
+        assert radii.is_floating_point()
+        _pos = _graph.pos if indices is None else _graph.pos[indices]
+        slices, j = self.grid.radius(_pos, radii.to(torch.float32))
+        i = indices if indices is not None else torch.arange(N)
+        return Selection(i.to(device), j.to(device), slices.to(device))
+
+    def getPointsInRangeSelection(self, radius: float, indices: torch.Tensor = None) -> Selection:
+        """Selector.py:232-233 (radius as a torch.float tensor over all points, as the reference builds it)."""
+        return self.getPointsInRangeSelectionVectorized(
+            torch.full((self.graph.num_nodes,), radius, dtype=torch.float, device=self.graph.pos.device), indices)
+
     def getKNNSelection(self, k: int, indices: torch.Tensor = None) -> Selection:
         _pos = self.graph.pos
         dev = _pos.device

@@ -150,6 +150,49 @@ __global__ void k_nn1(GridView g, const float* __restrict__ q, int64_t nq, float
     if (idx_out) idx_out[i] = tk.idx(0);
 }
 
+// ------------------------------------------------------------------ radius search (CPSD selection)
+// Selector.getPointsInRangeSelectionVectorized (Pointcloud/Modules/Selector.py:214-230): scipy query_ball_point on the
+// frozen f64 snapshot.  The membership test is scipy's own: ((dx² + dy²) + dz²) <= r² in float64 on the f32 inputs
+// (exact conversions), so the sets are identical, not just within a tolerance.  FILL = false counts per query,
+// FILL = true writes the members' ORIGINAL indices at out + off[q] (then sorted per query, scipy's order for
+// multi-point queries).
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_radius(GridView g, const float* __restrict__ q, int64_t nq,
+                                                 const float* __restrict__ radii, int64_t* __restrict__ count,
+                                                 const int64_t* __restrict__ off, int64_t* __restrict__ out) {
+    const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+    const double r = (double)radii[i];
+    const double r2 = r * r;
+    int64_t n = 0, w = FILL ? off[i] : 0;
+    if (r >= 0.0) {
+        // cells overlapping [q - r, q + r]; the f32 box is widened by one ulp-scale margin, the test is exact f64
+        const float rf = (float)(r * (1.0 + 1e-6)) + 1e-30f;
+        const int lo[3] = {max(cell_coord(qx - rf, g.ox, g.inv_h), 0), max(cell_coord(qy - rf, g.oy, g.inv_h), 0),
+                           max(cell_coord(qz - rf, g.oz, g.inv_h), 0)};
+        const int hi[3] = {min(cell_coord(qx + rf, g.ox, g.inv_h), g.dx - 1), min(cell_coord(qy + rf, g.oy, g.inv_h), g.dy - 1),
+                           min(cell_coord(qz + rf, g.oz, g.inv_h), g.dz - 1)};
+        for (int cz = lo[2]; cz <= hi[2]; ++cz)
+            for (int cy = lo[1]; cy <= hi[1]; ++cy)
+                for (int cx = lo[0]; cx <= hi[0]; ++cx) {
+                    uint32_t s, e;
+                    if (!cell_range(g, cx, cy, cz, s, e)) continue;
+                    for (uint32_t r0 = s; r0 < e; ++r0) {
+                        const float4 p = g.pts[r0];
+                        const double dx = (double)qx - (double)p.x, dy = (double)qy - (double)p.y,
+                                     dz = (double)qz - (double)p.z;
+                        const double d2 = __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
+                        if (d2 <= r2) {
+                            if (FILL) out[w++] = (int64_t)__float_as_uint(p.w);
+                            ++n;
+                        }
+                    }
+                }
+    }
+    if (!FILL) count[i] = n;
+}
+
 // K capacity ladder of the register top-k lists.
 static const int kCaps[] = {1, 4, 8, 13, 16, 32, 64};
 int knn_cap(int k) {
@@ -397,6 +440,42 @@ int pcd_knn(const pcd_grid* g, const float* q, int64_t nq, int k, void* idx_out,
     hipStream_t st = as_stream(stream);
     return sorted_ids ? launch_knn<false>(g->view, q, nq, kq, k, idx_out, idx_bits == 64, exclude_self, d2_out, st)
                       : launch_knn<true>(g->view, q, nq, kq, k, idx_out, idx_bits == 64, exclude_self, d2_out, st);
+}
+
+int pcd_radius_count(const pcd_grid* g, const float* q, int64_t nq, const float* radii, int64_t* counts,
+                     void* stream) {
+    PCD_CHECK_ARG(g != nullptr, "grid is null");
+    if (nq == 0) return PCD_OK;
+    PCD_CHECK_ARG(q && radii && counts, "null argument");
+    hipLaunchKernelGGL(k_radius<false>, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, as_stream(stream), g->view, q,
+                       nq, radii, counts, nullptr, nullptr);
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+int pcd_radius_fill(const pcd_grid* g, const float* q, int64_t nq, const float* radii, const int64_t* offsets,
+                    int64_t total, int64_t* idx_out, void* stream) {
+    PCD_CHECK_ARG(g != nullptr, "grid is null");
+    if (nq == 0 || total == 0) return PCD_OK;
+    PCD_CHECK_ARG(q && radii && offsets && idx_out, "null argument");
+    hipStream_t st = as_stream(stream);
+    int64_t* tmp_keys = nullptr;
+    void* tmp = nullptr;
+    size_t bytes = 0;
+    if (hipMalloc(&tmp_keys, total * sizeof(int64_t)) != hipSuccess) return fail(PCD_ERR_OOM, "radius fill temp");
+    hipLaunchKernelGGL(k_radius<true>, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, st, g->view, q, nq, radii,
+                       nullptr, offsets, tmp_keys);
+    // ascending original index within each query (scipy sorts multi-point query_ball_point results)
+    (void)rocprim::segmented_radix_sort_keys(nullptr, bytes, tmp_keys, idx_out, (unsigned int)total,
+                                             (unsigned int)nq, offsets, offsets + 1, 0, 64, st);
+    if (hipMalloc(&tmp, bytes) != hipSuccess) { (void)hipFree(tmp_keys); return fail(PCD_ERR_OOM, "radius sort temp"); }
+    hipError_t e = rocprim::segmented_radix_sort_keys(tmp, bytes, tmp_keys, idx_out, (unsigned int)total,
+                                                      (unsigned int)nq, offsets, offsets + 1, 0, 64, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(tmp);
+    (void)hipFree(tmp_keys);
+    if (e != hipSuccess) return fail(PCD_ERR_HIP, std::string("radius fill: ") + hipGetErrorString(e));
+    return PCD_OK;
 }
 
 int pcd_nn_dist(const pcd_grid* g, const float* q, int64_t nq, float* d2_out, int64_t* idx_out, void* stream) {

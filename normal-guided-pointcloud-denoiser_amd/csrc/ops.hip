@@ -36,6 +36,28 @@ __global__ __launch_bounds__(256) void k_nvt_csr(Rows3 pos, Rows3 nrm, const int
         for (int b = 0; b < 3; ++b) eigvec[9 * r + 3 * a + b] = V[a][b];
 }
 
+// CPSD tensors over a CSR selection (KIND 0: normal-filtered NVT, 1: normal-filtered PVT) + eigh.
+template <int KIND>
+__global__ __launch_bounds__(256) void k_cpsd_csr(Rows3 pos, Rows3 nrm, const int64_t* __restrict__ ci,
+                                                   const int64_t* __restrict__ off, const int64_t* __restrict__ nbr,
+                                                   int64_t m, float rho, float* __restrict__ eigval,
+                                                   float* __restrict__ eigvec) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    const int64_t s = off[r], e = off[r + 1];
+    const int64_t c = ci[r];
+    const Sym3 T = KIND == 0 ? nvt_normal_tensor(nrm, nrm(c), (int)(e - s), CsrNb{nbr, s}, rho)
+                             : pvt_normal_cov(pos, nrm, pos(c), nrm(c), (int)(e - s), CsrNb{nbr, s}, rho);
+    float w[3], V[3][3];
+    eigh3(T, w, V);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) eigval[3 * r + a] = w[a];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) eigvec[9 * r + 3 * a + b] = V[a][b];
+}
+
 __global__ void k_vu_smooth(const float* __restrict__ eigval, const float* __restrict__ eigvec, Rows3 n, int64_t m,
                             float tau, float damp, float* __restrict__ out) {
     const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -171,6 +193,28 @@ int pcd_nvt_csr(const float* pos, const float* n, int64_t npts, const int64_t* c
     PCD_CHECK_ARG(pos && n && ci && off && nbr && eigval && eigvec, "null argument");
     PCD_CHECK_ARG(npts > 0, "empty point set");
     hipLaunchKernelGGL(k_nvt_csr, dim3((unsigned)cdiv(m, 256)), dim3(256), 0, as_stream(stream), Rows3{pos},
+                       Rows3{n}, ci, off, nbr, m, rho, eigval, eigvec);
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+int pcd_nvt_normal_csr(const float* n, int64_t npts, const int64_t* ci, const int64_t* off, const int64_t* nbr,
+                       int64_t m, float rho, float* eigval, float* eigvec, void* stream) {
+    if (m == 0) return PCD_OK;
+    PCD_CHECK_ARG(n && ci && off && nbr && eigval && eigvec, "null argument");
+    PCD_CHECK_ARG(npts > 0, "empty point set");
+    hipLaunchKernelGGL(k_cpsd_csr<0>, dim3((unsigned)cdiv(m, 256)), dim3(256), 0, as_stream(stream), Rows3{n},
+                       Rows3{n}, ci, off, nbr, m, rho, eigval, eigvec);
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+int pcd_pvt_normal_csr(const float* pos, const float* n, int64_t npts, const int64_t* ci, const int64_t* off,
+                       const int64_t* nbr, int64_t m, float rho, float* eigval, float* eigvec, void* stream) {
+    if (m == 0) return PCD_OK;
+    PCD_CHECK_ARG(pos && n && ci && off && nbr && eigval && eigvec, "null argument");
+    PCD_CHECK_ARG(npts > 0, "empty point set");
+    hipLaunchKernelGGL(k_cpsd_csr<1>, dim3((unsigned)cdiv(m, 256)), dim3(256), 0, as_stream(stream), Rows3{pos},
                        Rows3{n}, ci, off, nbr, m, rho, eigval, eigvec);
     PCD_LAUNCH_CHECK();
     return PCD_OK;

@@ -92,6 +92,78 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho) {
     return T;
 }
 
+// ----------------------------------------------------------------- CPSD: Decompositionor.getNormalFilteredNVT
+// w_ij = acos(clamp(n_i . n_j, -1, 1)) <= rho (no abs, <=; Decompositionor.py:269); T_i = Σ w n_j n_jᵀ / Σ w;
+// a row where no neighbour votes gets n_i n_iᵀ (:273-275).  Sums in list order, like scatter_add.
+template <class Nr, class Nb>
+PCD_DEV Sym3 nvt_normal_tensor(Nr nrm, Vec3 ni, int cnt, Nb nb, float rho) {
+    float w00 = 0.f, w01 = 0.f, w02 = 0.f, w11 = 0.f, w12 = 0.f, w22 = 0.f;
+    int wsum = 0;
+    for (int t = 0; t < cnt; ++t) {
+        const Vec3 nj = nrm(nb(t));
+        const float c = fminf(fmaxf(dot3(ni, nj), -1.f), 1.f);
+        if (acosf(c) <= rho) {
+            w00 += nj.x * nj.x; w01 += nj.x * nj.y; w02 += nj.x * nj.z;
+            w11 += nj.y * nj.y; w12 += nj.y * nj.z; w22 += nj.z * nj.z;
+            ++wsum;
+        }
+    }
+    if (wsum == 0) return Sym3{ni.x * ni.x, ni.x * ni.y, ni.x * ni.z, ni.y * ni.y, ni.y * ni.z, ni.z * ni.z};
+    const float c = (float)wsum;
+    return Sym3{w00 / c, w01 / c, w02 / c, w11 / c, w12 / c, w22 / c};
+}
+
+// ----------------------------------------------------------------- CPSD: Decompositionor.getNormalFilteredPVT
+// Same vote; if none votes every w := 1 (:188-192).  c = Σ w v_j / Σ w, C = Σ w (v_j - c)(v_j - c)ᵀ / Σ w
+// (:194-200); an EMPTY neighbourhood gets Σ s sᵀ over s = ±(n × v), ±(n × (n × v)) (:201-208).
+PCD_DEV Vec3 cross3(Vec3 a, Vec3 b) {
+    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+template <class P, class Nr, class Nb>
+PCD_DEV Sym3 pvt_normal_cov(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float rho) {
+    if (cnt == 0) {
+        const Vec3 s1 = cross3(ni, vi), s2 = cross3(ni, s1);
+        const Vec3 sm[4] = {s1, -1.f * s1, s2, -1.f * s2};
+        float a[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {   // samples[:, :, None] * samples[..., None] summed over the 4 samples
+            a[0] += sm[u].x * sm[u].x; a[1] += sm[u].y * sm[u].x; a[2] += sm[u].z * sm[u].x;
+            a[3] += sm[u].y * sm[u].y; a[4] += sm[u].z * sm[u].y; a[5] += sm[u].z * sm[u].z;
+        }
+        return Sym3{a[0], a[1], a[2], a[3], a[4], a[5]};
+    }
+    int wsum = 0;
+    for (int t = 0; t < cnt; ++t) {
+        const float c = fminf(fmaxf(dot3(ni, nrm(nb(t))), -1.f), 1.f);
+        wsum += acosf(c) <= rho ? 1 : 0;
+    }
+    const bool all = wsum == 0;
+    if (all) wsum = cnt;
+    auto vote = [&](int64_t j) {
+        if (all) return true;
+        const float c = fminf(fmaxf(dot3(ni, nrm(j)), -1.f), 1.f);
+        return acosf(c) <= rho;
+    };
+    float sx = 0.f, sy = 0.f, sz = 0.f;
+    for (int t = 0; t < cnt; ++t) {
+        const int64_t j = nb(t);
+        if (!vote(j)) continue;
+        const Vec3 vj = pos(j);
+        sx += vj.x; sy += vj.y; sz += vj.z;
+    }
+    const float c = (float)wsum;
+    const Vec3 ctr = v3(sx / c, sy / c, sz / c);
+    float a00 = 0.f, a01 = 0.f, a02 = 0.f, a11 = 0.f, a12 = 0.f, a22 = 0.f;
+    for (int t = 0; t < cnt; ++t) {
+        const int64_t j = nb(t);
+        if (!vote(j)) continue;
+        const Vec3 d = pos(j) - ctr;   // T[a][b] = dv[b] * dv[a] (wij[...,None] * dv[:,None] * dv[...,None])
+        a00 += d.x * d.x; a01 += d.y * d.x; a02 += d.z * d.x;
+        a11 += d.y * d.y; a12 += d.z * d.y; a22 += d.z * d.z;
+    }
+    return Sym3{a00 / c, a01 / c, a02 / c, a11 / c, a12 / c, a22 / c};
+}
+
 // ----------------------------------------------------------------- H15: GraphBuilder.getPVTDecompositionWithKNN
 // C_i = Σ_j (v_j - v̄)(v_j - v̄)ᵀ with v̄ the mean of the k neighbours (GraphBuilder.py:105-110)
 template <class P, class Nb>

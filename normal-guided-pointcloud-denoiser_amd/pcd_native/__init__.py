@@ -51,6 +51,12 @@ _SIGS = {
     "pcd_grid_perm": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_knn": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pcd_knn_stats": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p]),
+    "pcd_radius_count": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "pcd_radius_fill": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "pcd_nvt_normal_csr": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p,
+                                   c_void_p, c_void_p]),
+    "pcd_pvt_normal_csr": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_float,
+                                   c_void_p, c_void_p, c_void_p]),
     "pcd_nvt_csr": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p,
                             c_void_p, c_void_p]),
     "pcd_vu_smooth": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p, c_void_p]),
@@ -208,6 +214,23 @@ class Grid:
         names = ["cells_considered", "cells_probed", "cells_found", "candidates", "inserts", "extra_rings"]
         return {nm: round(float(x), 2) for nm, x in zip(names, v)}
 
+    def radius(self, q: torch.Tensor, radii: torch.Tensor):
+        """Members of the ball of radii[i] around q[i] (original snapshot ids, ascending): (slices int64 [nq+1],
+        j int64 [total]) -- scipy query_ball_point semantics (pcd_radius_count / pcd_radius_fill)."""
+        q = f32(q)
+        r = f32(radii)
+        nq = q.size(0)
+        counts = torch.empty(nq, dtype=torch.int64, device=q.device)
+        check(lib().pcd_radius_count(self.handle, ptr(q), nq, ptr(r), ptr(counts), c_void_p(stream_ptr())),
+              "pcd_radius_count")
+        slices = torch.zeros(nq + 1, dtype=torch.int64, device=q.device)
+        torch.cumsum(counts, 0, out=slices[1:])
+        total = int(slices[-1])
+        j = torch.empty(total, dtype=torch.int64, device=q.device)
+        check(lib().pcd_radius_fill(self.handle, ptr(q), nq, ptr(r), ptr(slices), total, ptr(j),
+                                    c_void_p(stream_ptr())), "pcd_radius_fill")
+        return slices, j
+
     def nn(self, q: torch.Tensor):
         q = f32(q)
         d2 = torch.empty(q.size(0), dtype=torch.float32, device=q.device)
@@ -327,6 +350,24 @@ def nvt_csr(pos, n, ci, off, nbr, rho):
     evec = torch.empty((m, 3, 3), dtype=torch.float32, device=pos.device)
     check(lib().pcd_nvt_csr(ptr(pos), ptr(n), pos.size(0), ptr(ci), ptr(off), ptr(nbr), m, float(rho), ptr(ev),
                             ptr(evec), c_void_p(stream_ptr())), "pcd_nvt_csr")
+    return ev, evec
+
+
+def nvt_normal_csr(n, ci, off, nbr, rho):
+    m = ci.size(0)
+    ev = torch.empty((m, 3), dtype=torch.float32, device=n.device)
+    evec = torch.empty((m, 3, 3), dtype=torch.float32, device=n.device)
+    check(lib().pcd_nvt_normal_csr(ptr(n), n.size(0), ptr(ci), ptr(off), ptr(nbr), m, float(rho), ptr(ev),
+                                   ptr(evec), c_void_p(stream_ptr())), "pcd_nvt_normal_csr")
+    return ev, evec
+
+
+def pvt_normal_csr(pos, n, ci, off, nbr, rho):
+    m = ci.size(0)
+    ev = torch.empty((m, 3), dtype=torch.float32, device=pos.device)
+    evec = torch.empty((m, 3, 3), dtype=torch.float32, device=pos.device)
+    check(lib().pcd_pvt_normal_csr(ptr(pos), ptr(n), pos.size(0), ptr(ci), ptr(off), ptr(nbr), m, float(rho),
+                                   ptr(ev), ptr(evec), c_void_p(stream_ptr())), "pcd_pvt_normal_csr")
     return ev, evec
 
 

@@ -306,8 +306,48 @@ def gen_metrics(out_dir):
     print(f"metrics: CD mean {float(cd.mean()):.4g}")
 
 
+def gen_cpsd(out_dir):
+    """The CPSD ("Martin") feature path: radius selection (Selector.py:214-233, scipy query_ball_point on the frozen
+    f64 snapshot), getNormalFilteredNVT (Decompositionor.py:260-276), VU smoothing, getNormalFilteredPVT
+    (Decompositionor.py:172-211), getVUFeatures (:84-85), as composed by Processor.getMartinFeatureDecomposition
+    (Processor.py:102-108) and Processor.getVUDecomposition (Processor.py:83-100); plus corner_step on the CPSD
+    classes (the PostProcessing.ipynb:1041-1062 driver's corner phase)."""
+    f = np.load(os.path.join(out_dir, "fandisk_k32.npz"))
+    pos0 = torch.from_numpy(f["pos0"])
+    n0 = torch.from_numpy(f["n0"])
+    d = float(f["d"])
+    res = {"pos": f["pos0"], "n": f["n0"], "d": np.float64(d)}
+    proc = Processor(Pointcloud(pos0.clone(), n0.clone()))
+    for tag, r in (("r1", d), ("r2", 2 * d)):
+        sel = proc.selector.getPointsInRangeSelection(r)
+        res[f"sel_{tag}_radius"] = np.float64(r)
+        res[f"sel_{tag}_slices"] = sel.slices.numpy().astype(np.int64)
+        res[f"sel_{tag}_j"] = sel.j.numpy().astype(np.int32)
+    dec, fn = proc.getMartinFeatureDecomposition(r=d)
+    sel = proc.selector.getPointsInRangeSelection(d)
+    nvt = proc.decompositionor.getNormalFilteredNVT(sel, n0, 0.9)
+    res["nvt_eigval"] = np32(nvt.eigval)
+    res["nvt_eigvec"] = np32(nvt.eigvec)
+    res["f_n"] = np32(fn)
+    res["pvt_eigval"] = np32(dec.eigval)
+    res["pvt_eigvec"] = np32(dec.eigvec)
+    res["vu_classes"] = dec.getVUFeatures(tau=0.3).numpy().astype(np.int64)
+    sel8 = proc.selector.getKNNSelection(8)
+    corners = (dec.getVUFeatures(tau=0.3) == 2).nonzero().flatten()
+    res["corner_idx"] = corners.numpy().astype(np.int64)
+    res["corner_pos"] = np32(proc.denoiser.corner_step(sel8.filter(corners), fn, d * 20000, 1.0))
+    # Processor.getVUDecomposition: r = 2 * mean kNN(6, self excluded) edge length, rho = 0.95 for both votes
+    vu = proc.getVUDecomposition()
+    res["vud_eigval"] = np32(vu.eigval)
+    res["vud_eigvec"] = np32(vu.eigvec)
+    np.savez_compressed(os.path.join(out_dir, "cpsd.npz"), **res)
+    lens = np.diff(res["sel_r1_slices"])
+    print(f"cpsd: r={d:.5f} neighbours/pt {lens.mean():.1f} (min {lens.min()}, max {lens.max()}), "
+          f"VU classes {np.bincount(res['vu_classes'], minlength=3)}, corners {len(corners)}")
+
+
 GENS = {"fandisk": gen_fandisk, "steps": gen_steps, "lattice": gen_lattice, "mesh": gen_mesh,
-        "metrics": gen_metrics}
+        "metrics": gen_metrics, "cpsd": gen_cpsd}
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()

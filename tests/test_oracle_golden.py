@@ -175,3 +175,36 @@ def test_metrics(golden):
     m = golden("metrics")
     np.testing.assert_allclose(O.chamfer(m["a"], m["b"]), m["chamfer"], rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(O.paper_distance(m["a"], m["b"]), m["paper"], rtol=1e-5, atol=1e-9)
+
+
+# ------------------------------------------------------------------ CPSD path
+@pytest.fixture(scope="module")
+def cpsd(golden):
+    return golden("cpsd")
+
+
+@pytest.mark.parametrize("tag", ["r1", "r2"])
+def test_radius_selection_matches_reference(cpsd, tag):
+    slices, j = O.radius_selection(cpsd["pos"], cpsd["pos"], float(cpsd[f"sel_{tag}_radius"]))
+    np.testing.assert_array_equal(slices, cpsd[f"sel_{tag}_slices"])
+    np.testing.assert_array_equal(j, cpsd[f"sel_{tag}_j"])
+
+
+def test_martin_feature_decomposition_matches_reference(cpsd):
+    pos, n, d = cpsd["pos"], cpsd["n"], float(cpsd["d"])
+    slices, j = O.radius_selection(pos, pos, d)
+    ci = np.arange(len(pos))
+    w1, _ = O.normal_filtered_nvt(n, ci, slices, j, 0.9)
+    np.testing.assert_allclose(w1, cpsd["nvt_eigval"], atol=2e-6)
+    w2, v2, fn = O.martin_feature_decomposition(pos, pos, n, d, 0.9)
+    ang = angle64(fn, cpsd["f_n"])
+    assert ang.max() < 1e-6
+    scale = np.abs(cpsd["pvt_eigval"]).max(1, keepdims=True) + 1e-30
+    assert (np.abs(w2 - cpsd["pvt_eigval"]) / scale).max() < 1e-5
+    np.testing.assert_array_equal(O.vu_features(w2, 0.3), cpsd["vu_classes"])
+
+
+def angle64(a, b):
+    """Angle between row vectors in float64 (arccos of an f32 dot cannot resolve below ~5e-4 rad)."""
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.arctan2(np.linalg.norm(np.cross(a, b), axis=1), (a * b).sum(1))
