@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restri
 // Writes the anchor, its list and the kstore-column kNN list.
 // DENSE: every active row (no anchors yet); else the rows on the redo list.  Grid-stride over waves.
 template <int KA, bool DENSE>
-__global__ __launch_bounds__(256) void k_knn_redo_wave(GridView g, const float4* __restrict__ pos, int64_t N, RowMap rm,
+__global__ __launch_bounds__(256, 4) void k_knn_redo_wave(GridView g, const float4* __restrict__ pos, int64_t N, RowMap rm,
                                                         int kstore, float4* __restrict__ anc,
                                                         int32_t* __restrict__ alist, int32_t* __restrict__ idx,
                                                         const int32_t* __restrict__ redo,

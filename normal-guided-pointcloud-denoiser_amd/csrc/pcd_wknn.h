@@ -3,8 +3,8 @@
 // The lane-per-query searches (pcd_knn.h) keep a sorted top-K in each lane's registers; at K = 64 that list is 128
 // VGPRs and every accepted candidate runs a 64-step select chain, so a sparse set of queries (the 1-3 % that fail
 // the anchor test) runs at 2 waves/SIMD on long serial chains.  Here the 64 lanes split one query's work instead:
-//   1. the cells of the box [q - r, q + r] (r = sqrt of the acceptance cap) are dealt one per lane, pruned by
-//      box distance and probed in the hash table in parallel;
+//   1. the cells of the box [q - r, q + r] (r = sqrt of the acceptance cap) are dealt 4 per lane, pruned by
+//      box distance and probed in the brick hash in parallel (all probes of a chunk in flight together);
 //   2. the chunk's candidate rows are flattened (count scan in LDS, binary-searched per row) and dealt kWaveRows
 //      per lane per round, all
 //      loads of a round in flight together; a key (d² bits << 32 | rank) below the cap is appended to the wave's
@@ -111,9 +111,12 @@ PCD_DEV unsigned long long wave_sort_survivors(unsigned long long* buf, int cnt,
     return top;
 }
 
-struct WaveCells {          // per-wave LDS scratch for one chunk of <= 64 cells
-    uint32_t start[64];
-    uint32_t end_incl[64];  // inclusive scan of the counts: flattened candidate end of each cell
+static constexpr int kCellsPerLane = 2;                 // cells per lane per chunk
+static constexpr int kChunkCells = 64 * kCellsPerLane;  // cells per chunk
+static constexpr int kChunkLog2 = kCellsPerLane == 1 ? 6 : kCellsPerLane == 2 ? 7 : kCellsPerLane == 4 ? 8 : 9;
+struct WaveCells {          // per-wave LDS scratch for one chunk of cells
+    uint32_t start[kChunkCells];
+    uint32_t end_incl[kChunkCells];  // inclusive scan of the counts: flattened candidate end of each cell
 };
 
 // Append the keys < cap of one candidate row per lane to the wave's survivor buffer (one ballot compaction).
@@ -124,10 +127,11 @@ PCD_DEV void wave_append(bool pass, unsigned long long key, unsigned long long* 
 }
 
 // Scan the cells of box [lo, hi] (cell coords), appending keys < cap to buf.  cap may tighten (buffer reduce).
-// Latency-shaped: one round of hash probes per chunk of 64 cells, then the chunk's flattened candidate rows in
-// rounds of kWaveRows per lane -- every row index first (binary search of the count scan in LDS), then all the
-// point loads at once, then the keys -- so a query costs a handful of dependent memory round trips.
-static constexpr int kWaveRows = 8;
+// Latency-shaped: a chunk is up to 256 cells (the whole cap box of a typical query), kCellsPerLane per lane, whose
+// brick-hash probes, then brick-block loads, are each issued together (two memory round trips for the chunk);
+// then the chunk's flattened candidate rows in rounds of kWaveRows per lane -- every row index first (binary search
+// of the count scan in LDS), then all the point loads at once, then the keys.
+static constexpr int kWaveRows = 4;
 template <int K>
 PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int hi[3], unsigned long long& cap,
                            unsigned long long* buf, int& cnt, WaveCells* wc, int lane) {
@@ -137,25 +141,66 @@ PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int
     const int64_t nc = (int64_t)ex * ey * ez;
     const bool small = nc < (1ll << 31);
     const uint32_t exy = (uint32_t)ex * (uint32_t)ey;
-    for (int64_t base = 0; base < nc; base += 64) {
-        uint32_t s = 0, e = 0;
-        const int64_t ci = base + lane;
-        if (ci < nc) {
-            int cx, cy, cz;
-            if (small) {
-                const uint32_t c32 = (uint32_t)ci, zq = c32 / exy, rem = c32 - zq * exy, yq = rem / (uint32_t)ex;
-                cx = lo[0] + (int)(rem - yq * (uint32_t)ex); cy = lo[1] + (int)yq; cz = lo[2] + (int)zq;
-            } else {
-                cx = lo[0] + (int)(ci % ex); cy = lo[1] + (int)((ci / ex) % ey); cz = lo[2] + (int)(ci / ((int64_t)ex * ey));
-            }
-            const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
-            const float gx = axis_gap(q.x, lx, lx + g.h), gy = axis_gap(q.y, ly, ly + g.h), gz = axis_gap(q.z, lz, lz + g.h);
-            const float kth = __uint_as_float((unsigned)(cap >> 32));
-            if (gx * gx + gy * gy + gz * gz <= kth * 1.00001f + 1e-30f) {
-                if (!cell_range(g, cx, cy, cz, s, e)) s = e = 0;
+    for (int64_t base = 0; base < nc; base += kChunkCells) {
+        // 1. this lane's cells (lane-major: cells lane*CPL .. +CPL-1 of the chunk): prune, hash slot, probe
+        unsigned long long key[kCellsPerLane], slot[kCellsPerLane];
+        bool want[kCellsPerLane];
+        uint4 sl[kCellsPerLane];
+        const float kth = __uint_as_float((unsigned)(cap >> 32));
+#pragma unroll
+        for (int u = 0; u < kCellsPerLane; ++u) {
+            const int64_t ci = base + lane * kCellsPerLane + u;
+            want[u] = false;
+            key[u] = 0; slot[u] = 0;
+            if (ci < nc) {
+                int cx, cy, cz;
+                if (small) {
+                    const uint32_t c32 = (uint32_t)ci, zq = c32 / exy, rem = c32 - zq * exy, yq = rem / (uint32_t)ex;
+                    cx = lo[0] + (int)(rem - yq * (uint32_t)ex); cy = lo[1] + (int)yq; cz = lo[2] + (int)zq;
+                } else {
+                    cx = lo[0] + (int)(ci % ex); cy = lo[1] + (int)((ci / ex) % ey); cz = lo[2] + (int)(ci / ((int64_t)ex * ey));
+                }
+                const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
+                const float gx = axis_gap(q.x, lx, lx + g.h), gy = axis_gap(q.y, ly, ly + g.h), gz = axis_gap(q.z, lz, lz + g.h);
+                if (gx * gx + gy * gy + gz * gz <= kth * 1.00001f + 1e-30f) {
+                    want[u] = true;
+                    key[u] = morton3(cx, cy, cz);
+                    slot[u] = hash_slot(key[u] >> 6, g.hbits);
+                }
             }
         }
-        uint32_t incl = e - s;
+#pragma unroll
+        for (int u = 0; u < kCellsPerLane; ++u)
+            sl[u] = want[u] ? *reinterpret_cast<const uint4*>(g.table + slot[u]) : make_uint4(~0u, ~0u, 0u, 0u);
+        // 2. resolve the probes (linear probing past a collision is rare), then the brick blocks, all in flight
+        uint32_t brick[kCellsPerLane];
+#pragma unroll
+        for (int u = 0; u < kCellsPerLane; ++u) {
+            brick[u] = ~0u;
+            if (!want[u]) continue;
+            const unsigned long long bkey = key[u] >> 6;
+            uint4 e = sl[u];
+            unsigned long long sidx = slot[u];
+            for (;;) {
+                const unsigned long long k2 = (unsigned long long)e.x | ((unsigned long long)e.y << 32);
+                if (k2 == bkey) { brick[u] = e.z; break; }
+                if (k2 == kEmptyKey) break;
+                sidx = (sidx + 1) & g.mask;
+                e = *reinterpret_cast<const uint4*>(g.table + sidx);
+            }
+        }
+        uint2 cr[kCellsPerLane];
+#pragma unroll
+        for (int u = 0; u < kCellsPerLane; ++u)
+            cr[u] = brick[u] != ~0u ? g.cells[(uint64_t)brick[u] * 64 + (key[u] & 63)] : make_uint2(0u, 0u);
+        // 3. counts -> lane-local prefix -> wave exclusive scan of the lane totals
+        uint32_t loc[kCellsPerLane], run = 0;
+#pragma unroll
+        for (int u = 0; u < kCellsPerLane; ++u) {
+            run += cr[u].y > cr[u].x ? cr[u].y - cr[u].x : 0u;
+            loc[u] = run;
+        }
+        uint32_t incl = run;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
@@ -165,9 +210,13 @@ PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int
         PCD_WSTAT(1, 1);
         PCD_WSTAT(2, total);
         if (total == 0) continue;
+        const uint32_t excl = incl - run;
         wave_sync();                         // the previous chunk's readers are done with wc
-        wc->start[lane] = s;
-        wc->end_incl[lane] = incl;
+#pragma unroll
+        for (int u = 0; u < kCellsPerLane; ++u) {
+            wc->start[lane * kCellsPerLane + u] = cr[u].x;
+            wc->end_incl[lane * kCellsPerLane + u] = excl + loc[u];
+        }
         wave_sync();
         for (uint32_t j0 = 0; j0 < total; j0 += 64 * kWaveRows) {
             uint32_t r[kWaveRows];
@@ -176,9 +225,9 @@ PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int
                 const uint32_t j = j0 + (uint32_t)(u * 64 + lane);
                 r[u] = 0u;
                 if (j0 + (uint32_t)(u * 64) >= total) continue;   // wave-uniform: slot past the chunk
-                int a = 0, b = 63;           // first cell whose inclusive end exceeds j
+                int a = 0, b = kChunkCells - 1;   // first cell whose inclusive end exceeds j
 #pragma unroll
-                for (int it = 0; it < 6; ++it) {
+                for (int it = 0; it < kChunkLog2; ++it) {
                     const int m = (a + b) >> 1;
                     if (wc->end_incl[m] > j) b = m; else a = m + 1;
                 }
@@ -200,8 +249,8 @@ PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int
                         if (kept == K && kth_key + 1ull < cap) cap = kth_key + 1ull;
                         cnt = kept;
                     }
-                    const unsigned long long key = cand_key<false>(q, p[u], r[u]);
-                    wave_append(j < total && key < cap, key, buf, cnt, lane);
+                    const unsigned long long key2 = cand_key<false>(q, p[u], r[u]);
+                    wave_append(j < total && key2 < cap, key2, buf, cnt, lane);
                 }
             }
             wave_sync();
