@@ -26,6 +26,8 @@
  *   pcd_denoiser_*                  Processor.denoise / getMyFeatureDecomposition / denoiseUntilMinimumError loop body
  *                                                                              Pointcloud/Modules/Processor.py:110-185
  *   pcd_orient_normals_mst          GraphBuilder.flipNormals (MST + DFS, host) Pointcloud/Modules/GraphBuilder.py:129-209
+ *   pcd_orient_normals_mst_gpu      GraphBuilder.flipNormals (Borůvka MST + Euler-tour rooting + sign pointer jumping,
+ *                                   device)                                    Pointcloud/Modules/GraphBuilder.py:129-209
  */
 #ifndef PCD_H
 #define PCD_H
@@ -221,6 +223,13 @@ int pcd_denoiser_unpack(pcd_denoiser* dn, int field, const int32_t* rows, int64_
  * n [npts][3] fp32 modified in place. */
 int pcd_orient_normals_mst(const float* pos, float* n, int64_t npts, const int64_t* a, const int64_t* b,
                            int64_t e);
+/* Same contract and bit-identical result on DEVICE memory (pos [npts][3], n [npts][3] in place, a/b [e] int64),
+ * ordered on `stream`; synchronises the stream before returning.  The minimum spanning forest is unique under
+ * keys (cost, edge index), which is the host's stable Kruskal order, and each node's sign is a composition of
+ * per-edge maps {identity, negate, +1} from the root's sign, so the DFS visit order never matters.
+ * PCD_ERR_ARG for an out-of-range edge index; npts and e must be < 2^32. */
+int pcd_orient_normals_mst_gpu(const float* pos, float* n, int64_t npts, const int64_t* a, const int64_t* b,
+                               int64_t e, void* stream);
 
 /* ------------------------------------------------------------------ host builds of the per-point math */
 /* The exact __host__ __device__ code the kernels run, compiled for the CPU (HOST pointers); for tests.

@@ -2,8 +2,9 @@
 
 getKNNEdgeIndex(k) -> kNN of the CURRENT positions over a fresh grid, self excluded (torch_cluster.knn_graph,
 flow="target_to_source", GraphBuilder.py:60-63); getPVTDecompositionWithKNN -> pcd_pca_dense (covariance about the
-neighbours' mean + Jacobi eigh, :99-111); flipNormals -> pcd_orient_normals_mst (Kruskal MST + DFS on the host,
-:129-209).
+neighbours' mean + Jacobi eigh, :99-111); flipNormals -> pcd_orient_normals_mst_gpu (Borůvka MST + Euler-tour
+rooting + sign pointer jumping on the device, :129-209; bit-identical to the host Kruskal + DFS pcd_orient_normals_mst,
+which the tests keep as the cross-check).
 """
 from __future__ import annotations
 
@@ -63,11 +64,9 @@ class GraphBuilder:
         _graph.edge_attr = 1 - (normals[0] * normals[1]).sum(dim=-1).abs_()
 
     def flipNormals(self) -> None:
-        """MST over 1-|n_i·n_j| then DFS sign propagation from the highest point (host C++, libpcd)."""
+        """MST over 1-|n_i·n_j| then sign propagation from the highest point (GraphBuilder.py:129-209), on the GPU."""
         _graph = self.graph
         GeneralUtils.validateAttributes(_graph, ["pos", "n", "edge_index"])
-        pos = _graph.pos.detach().to("cpu", torch.float32).contiguous()
-        n = _graph.n.detach().to("cpu", torch.float32).contiguous().clone()
-        ei = _graph.edge_index.detach().to("cpu", torch.int64)
-        _nat.orient_normals_mst(pos, n, ei[0].contiguous(), ei[1].contiguous())
-        _graph.n = n.to(_graph.pos.device)
+        ei = _graph.edge_index.detach()
+        n = _nat.orient_normals_mst_gpu(_graph.pos.detach(), _graph.n.detach(), ei[0], ei[1])
+        _graph.n = n.to(device=_graph.pos.device, dtype=_graph.pos.dtype)

@@ -85,6 +85,7 @@ _SIGS = {
     "pcd_denoiser_unpack": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "pcd_denoiser_get_timing": (c_int, [c_void_p, POINTER(c_float), c_int, POINTER(c_int)]),
     "pcd_orient_normals_mst": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64]),
+    "pcd_orient_normals_mst_gpu": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p]),
     "pcd_host_eigh3": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "pcd_host_vu_smooth": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p]),
     "pcd_host_solve3": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
@@ -462,3 +463,16 @@ def orient_normals_mst(pos_host, n_host, a_host, b_host):
     assert not pos_host.is_cuda and not n_host.is_cuda
     check(lib().pcd_orient_normals_mst(ptr(pos_host), ptr(n_host), pos_host.size(0), ptr(a_host), ptr(b_host),
                                        a_host.size(0)), "pcd_orient_normals_mst")
+
+
+def orient_normals_mst_gpu(pos, n, a, b) -> torch.Tensor:
+    """Device MST orientation (Borůvka + Euler tour + sign pointer jumping), bit-identical to the host version.
+    Returns the oriented normals as a new device f32 tensor; the inputs are not modified."""
+    p = f32(pos)
+    out = f32(n).clone()
+    a = i64(a).reshape(-1)
+    b = i64(b).reshape(-1)
+    assert p.dim() == 2 and p.size(1) == 3 and out.shape == p.shape and a.numel() == b.numel()
+    check(lib().pcd_orient_normals_mst_gpu(ptr(p), ptr(out), p.size(0), ptr(a), ptr(b), a.numel(),
+                                           c_void_p(stream_ptr())), "pcd_orient_normals_mst_gpu")
+    return out
