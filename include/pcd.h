@@ -236,6 +236,10 @@ int pcd_orient_normals_mst_gpu(const float* pos, float* n, int64_t npts, const i
  *   t6 [m][6] = (a00, a01, a02, a11, a12, a22) -> w [m][3] ascending, v [m][3][3] columns (LAPACK ssyevd signs) */
 int pcd_host_eigh3(const float* t6, int64_t m, float* w, float* v);
 int pcd_host_vu_smooth(const float* w, const float* v, const float* n, int64_t m, float tau, float damp, float* out);
+/* getBetterFilteredNVT's tensor T (before eigh) for CSR rows: centres ci [m], neighbours nbr[off[r] .. off[r+1]),
+ * pos / n [.][3] -> t6 [m][6] (a00, a01, a02, a11, a12, a22); the fused kernels' vote and sums, on the host. */
+int pcd_host_nvt_tensor(const float* pos, const float* n, const int64_t* ci, const int64_t* off, const int64_t* nbr,
+                        int64_t m, float rho, float* t6);
 /* a9 [m][3][3] row-major, b3 [m][3] -> x3 [m][3], ok [m] (0 when a pivot is exactly zero, x untouched = 0) */
 int pcd_host_solve3(const float* a9, const float* b3, int64_t m, float* x3, int32_t* ok);
 

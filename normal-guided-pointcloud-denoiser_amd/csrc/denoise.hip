@@ -40,7 +40,50 @@ struct ColNbStream {
     int64_t n, i;
     PCD_DEV int64_t operator()(int t) const { return __builtin_nontemporal_load(idx + (int64_t)t * n + i); }
 };
+// A column-major list re-read from memory with out-of-range entries mapped to the row itself (the fallback pass
+// of nvt_tensor; an invalid entry is already reported by the kernel's own check).
+struct ColNbSafe {
+    const int32_t* idx;
+    int64_t n, i;
+    PCD_DEV int64_t operator()(int t) const {
+        const int64_t j = idx[(int64_t)t * n + i];
+        return (uint64_t)j < (uint64_t)n ? j : i;
+    }
+};
 typedef float v4f __attribute__((ext_vector_type(4)));
+
+// LDS window of per-point rows.  The rows are in spatial order, so the neighbours of a block's 256 consecutive rows
+// mostly lie within a few hundred rows of them (~90 % within +-256 on scanned surfaces): the block stages that
+// window of two row arrays into LDS with coalesced loads, and each neighbour gather reads LDS when it falls inside
+// (one ds_read_b128) and global memory otherwise (a global load for those lanes only).  A wave's divergent 16-B
+// gathers cost the texture-address unit ~1 cycle per distinct cache line, ~35 cycles per instruction -- the
+// measured limiter of the NVT kernels (TA busy 65-77 %); LDS serves them in a few.
+static constexpr int kWinHalo = 256;                   // rows staged on either side of the block's own rows
+static constexpr int kWinRows = 256 + 2 * kWinHalo;    // rows per array in the window (12 KB each)
+struct WinRows {
+    const float4* g;
+    const float4* s;
+    int64_t lo;
+    PCD_DEV Vec3 operator()(int64_t j) const {
+        const uint64_t o = (uint64_t)(j - lo);
+        float4 q;
+        if (o < (uint64_t)kWinRows) q = s[o];
+        else q = g[j];
+        return v3(q.x, q.y, q.z);
+    }
+};
+// Stage rows [lo, lo + kWinRows) of a and b (clipped to [0, N)) for the block whose first active row is i_first.
+PCD_DEV int64_t stage_window(const float4* __restrict__ a, const float4* __restrict__ b, int64_t N, int64_t i_first,
+                             float4* sa, float4* sb) {
+    int64_t lo = i_first - kWinHalo;
+    lo = lo < 0 ? 0 : lo;
+    for (int r = threadIdx.x; r < kWinRows; r += blockDim.x) {
+        const int64_t j = lo + r;
+        if (j < N) { sa[r] = a[j]; sb[r] = b[j]; }
+    }
+    __syncthreads();
+    return lo;
+}
 struct RegNb32 {
     const int* l;
     PCD_DEV int64_t operator()(int t) const { return l[t]; }
@@ -109,7 +152,7 @@ PCD_DEV void k1_epilogue(const float4* __restrict__ pos, const float4* __restric
     const float4 n4 = nrm[i];
     __builtin_nontemporal_store(v4f{n4.x, n4.y, n4.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
 #else
-    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho);
+    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho, ColNbSafe{idx, N, i});
     const float4 n4 = nrm[i];
     float w[3], V[3][3];
     eigh3(T, w, V);
@@ -235,7 +278,10 @@ __global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restri
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                int kstore, float rho, float tau, float damp, Cover cov,
                                                float4* __restrict__ fn, int* __restrict__ err) {
-    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    __shared__ float4 s_pos[kWinRows], s_nrm[kWinRows];
+    const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
+    const int64_t lo = stage_window(pos, nrm, N, rm(b0), s_pos, s_nrm);
+    const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 p4 = pos[i];
@@ -255,7 +301,8 @@ __global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restri
             if (t == kstore - 1) dk = dist2(vi, g.pts[l[t]]);
         if (!cov.holds(vi, dk)) atomicOr(err, 2);
     }
-    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho);
+    const Sym3 T = nvt_tensor<K>(WinRows{pos, s_pos, lo}, WinRows{nrm, s_nrm, lo}, vi, k, RegNb32{l}, rho,
+                                 ColNbSafe{idx, N, i});
     float w[3], V[3][3];
     eigh3(T, w, V);
     const float4 n4 = nrm[i];
@@ -303,11 +350,15 @@ __global__ __launch_bounds__(256) void k_nvt2(const float4* __restrict__ pos, co
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                float rho, float scale, uint8_t* __restrict__ cls,
                                                float4* __restrict__ edge) {
-    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    __shared__ float4 s_pos[kWinRows], s_fn[kWinRows];
+    const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
+    const int64_t lo = stage_window(pos, fn, N, rm(b0), s_pos, s_fn);
+    const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 p4 = pos[i];
-    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{fn}, v3(p4.x, p4.y, p4.z), k, ColNbStream{idx, N, i}, rho);
+    const Sym3 T = nvt_tensor<K>(WinRows{pos, s_pos, lo}, WinRows{fn, s_fn, lo}, v3(p4.x, p4.y, p4.z), k,
+                                 ColNbStream{idx, N, i}, rho, ColNbSafe{idx, N, i});
     float w[3], V[3][3];
     eigh3(T, w, V);
     cls[i] = (uint8_t)classify(w, scale, nullptr);

@@ -1,9 +1,17 @@
 // Host builds of the per-point math (the same __host__ __device__ source the kernels use), exported so the CPU
 // test-suite can check eigen-decomposition signs, VU smoothing and the 3x3 solve without a GPU.
 #include "pcd_host.h"
-#include "pcd_device.h"
+#include "pcd_ops.h"
 
 using namespace pcd;
+
+namespace {
+struct HostCsrNb {
+    const int64_t* nbr;
+    int64_t base;
+    int64_t operator()(int t) const { return nbr[base + t]; }
+};
+}  // namespace
 
 extern "C" {
 
@@ -42,6 +50,18 @@ int pcd_host_solve3(const float* a9, const float* b3, int64_t m, float* x3, int3
         Vec3 x = v3(0.f, 0.f, 0.f);
         ok[i] = solve3(A, v3(b3[3 * i], b3[3 * i + 1], b3[3 * i + 2]), x) ? 1 : 0;
         x3[3 * i] = x.x; x3[3 * i + 1] = x.y; x3[3 * i + 2] = x.z;
+    }
+    return PCD_OK;
+}
+
+int pcd_host_nvt_tensor(const float* pos, const float* n, const int64_t* ci, const int64_t* off, const int64_t* nbr,
+                        int64_t m, float rho, float* t6) {
+    PCD_CHECK_ARG(pos && n && ci && off && (m == 0 || nbr) && t6, "null argument");
+    for (int64_t r = 0; r < m; ++r) {
+        const Sym3 T = nvt_tensor(Rows3{pos}, Rows3{n}, Rows3{pos}(ci[r]), (int)(off[r + 1] - off[r]),
+                                  HostCsrNb{nbr, off[r]}, rho);
+        float* o = t6 + 6 * r;
+        o[0] = T.a00; o[1] = T.a01; o[2] = T.a02; o[3] = T.a11; o[4] = T.a12; o[5] = T.a22;
     }
     return PCD_OK;
 }

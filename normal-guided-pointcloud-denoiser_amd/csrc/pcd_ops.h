@@ -41,33 +41,38 @@ PCD_DEV void for_neighbours(P pos, Nr nrm, int cnt, Nb nb, F&& f) {
 // UNROLL > 0: the neighbour loop is fully unrolled to UNROLL (>= cnt) so register-resident neighbour lists stay
 // in registers and every gather of the list can be issued before the first is consumed.
 //
-// The binary vote is decided on a fast estimate of c (hardware sqrt / reciprocal instead of the IEEE sqrt, three
-// divisions and acos) whenever the estimate is farther from the threshold cos(rho) than its error bound; only the
-// rare pairs within that margin (or with a degenerate |dv|²) evaluate the reference expression exactly.  Since
-// acos is monotone, the vote is the same either way: the estimate's error is ~1e-6 (|dn| <= 1, 1-ulp hardware
-// ops), the margin 4e-6·(1 + |n_j|₁), and cos(rho) vs acos's own rounding differ by < 1e-6.
-template <int UNROLL = 0, class P, class Nr, class Nb>
-PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho) {
+// The binary vote is decided without sqrt, divisions or acos whenever that is safe: with e = dv . n_j and
+// sq = |dv|², the reference's |c| < cos(rho) is e² < cos²(rho)·sq (cos(rho) > 0; for rho >= π/2 no pair votes, and
+// cos² is taken as -1 so that none does).  Only pairs with |e² - cos²(rho)·sq| <= 4e-6·(1 + |n_j|₁)²·sq, or with
+// sq outside [1e-24, 1e30] (where F.normalize's eps or over/underflow matter), evaluate the reference expression
+// exactly; sq = 0 (the row's own entry: the snapshot point of a row is its current point's neighbour) has the
+// constant vote acos(0) > rho.  The margin covers the estimate's error: |c_est - c_ref| ~ 1e-6 and cos(rho) vs acos's own rounding
+// < 1e-6 give |c_est - cos(rho)| > 4e-6·(1 + |n_j|₁) whenever the squared test clears its margin, since
+// |c| + cos(rho) <= 1 + |n_j|₁; e² and cos²(rho)·sq are themselves within ~1e-7 of that scale.
+// Sums: the voting neighbours' n_j n_jᵀ in list order (the weight folded into one factor: w·n_j, exact).  The
+// all-ones fallback (no vote) re-reads the rows and sums every n_j n_jᵀ in list order -- a rare row.
+// nbf: the same list for the rare fallback pass (a memory-backed accessor, so register-resident lists need not
+// stay live across the vote loop).
+template <int UNROLL = 0, class P, class Nr, class Nb, class NbF>
+PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF nbf) {
     float w00 = 0.f, w01 = 0.f, w02 = 0.f, w11 = 0.f, w12 = 0.f, w22 = 0.f;
-    float u00 = 0.f, u01 = 0.f, u02 = 0.f, u11 = 0.f, u12 = 0.f, u22 = 0.f;
     int wsum = 0;
     const float cthr = cosf(rho);
+    const float cthr2 = cthr > 0.f ? cthr * cthr : -1.f;
+    const bool w_self = acosf(0.f) > rho;   // the vote of a coincident neighbour (every row lists itself)
     auto body2 = [&](const Vec3 vj, const Vec3 nj) {
         const Vec3 dv = vj - vi;
 #if defined(PCD_EXP_NOVOTE)
         const bool w = dv.x > 0.f;
 #else
         const float sq = sq3(dv);
-#ifdef __HIP_DEVICE_COMPILE__
-        const float inv = __builtin_amdgcn_rcpf(fmaxf(__builtin_amdgcn_sqrtf(sq), 1e-12f));
-#else
-        const float inv = 1.f / fmaxf(sqrtf(sq), 1e-12f);
-#endif
-        float ca = (dv.x * inv * nj.x + dv.y * inv * nj.y) + dv.z * inv * nj.z;
-        ca = fabsf(fminf(fmaxf(ca, -1.f), 1.f));
-        const float marg = 4e-6f * (1.f + fabsf(nj.x) + fabsf(nj.y) + fabsf(nj.z));
-        bool w = ca < cthr;
-        if (!(fabsf(ca - cthr) > marg) || !(sq > 1e-30f && sq < 1e30f)) {   // near the threshold: exact
+        const float e = (dv.x * nj.x + dv.y * nj.y) + dv.z * nj.z;
+        const float lhs = e * e, rhs = cthr2 * sq;
+        const float n1 = 1.f + fabsf(nj.x) + fabsf(nj.y) + fabsf(nj.z);
+        bool w = lhs < rhs;
+        if (sq == 0.f) {
+            w = w_self;                      // the row itself (dv = 0): normalize gives 0, c = 0
+        } else if (!(fabsf(lhs - rhs) > 4e-6f * n1 * n1 * sq) || !(sq >= 1e-24f && sq < 1e30f)) {   // near: exact
             const float den = fmaxf(sqrtf(sq), 1e-12f);
             const Vec3 dn = v3(dv.x / den, dv.y / den, dv.z / den);
             float c = dot3(dn, nj);
@@ -75,21 +80,28 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho) {
             w = acosf(c) > rho;
         }
 #endif
-        const float o00 = nj.x * nj.x, o01 = nj.x * nj.y, o02 = nj.x * nj.z;
-        const float o11 = nj.y * nj.y, o12 = nj.y * nj.z, o22 = nj.z * nj.z;
-        u00 += o00; u01 += o01; u02 += o02; u11 += o11; u12 += o12; u22 += o22;
-        if (w) { w00 += o00; w01 += o01; w02 += o02; w11 += o11; w12 += o12; w22 += o22; ++wsum; }
+        const Vec3 nw = w ? nj : v3(0.f, 0.f, 0.f);
+        w00 += nw.x * nj.x; w01 += nw.x * nj.y; w02 += nw.x * nj.z;
+        w11 += nw.y * nj.y; w12 += nw.y * nj.z; w22 += nw.z * nj.z;
+        wsum += w ? 1 : 0;
     };
     for_neighbours<UNROLL>(pos, nrm, cnt, nb, body2);
-    Sym3 T;
     if (wsum == 0) {
-        const float c = (float)cnt;
-        T = Sym3{u00 / c, u01 / c, u02 / c, u11 / c, u12 / c, u22 / c};
-    } else {
-        const float c = (float)wsum;
-        T = Sym3{w00 / c, w01 / c, w02 / c, w11 / c, w12 / c, w22 / c};
+        w00 = w01 = w02 = w11 = w12 = w22 = 0.f;
+#pragma unroll 1
+        for (int t = 0; t < cnt; ++t) {
+            const Vec3 nj = nrm(nbf(t));
+            w00 += nj.x * nj.x; w01 += nj.x * nj.y; w02 += nj.x * nj.z;
+            w11 += nj.y * nj.y; w12 += nj.y * nj.z; w22 += nj.z * nj.z;
+        }
+        wsum = cnt;
     }
-    return T;
+    const float c = (float)wsum;
+    return Sym3{w00 / c, w01 / c, w02 / c, w11 / c, w12 / c, w22 / c};
+}
+template <int UNROLL = 0, class P, class Nr, class Nb>
+PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho) {
+    return nvt_tensor<UNROLL>(pos, nrm, vi, cnt, nb, rho, nb);
 }
 
 // ----------------------------------------------------------------- CPSD: Decompositionor.getNormalFilteredNVT

@@ -89,6 +89,7 @@ _SIGS = {
     "pcd_host_eigh3": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "pcd_host_vu_smooth": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p]),
     "pcd_host_solve3": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "pcd_host_nvt_tensor": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p]),
 }
 
 _lib = None
@@ -445,6 +446,18 @@ def host_vu_smooth(w, v, n, tau=0.3, damp=3.0):
     out = np.empty_like(n)
     check(lib().pcd_host_vu_smooth(w.ctypes.data, v.ctypes.data, n.ctypes.data, n.shape[0], float(tau), float(damp),
                                    out.ctypes.data), "pcd_host_vu_smooth")
+    return out
+
+
+def host_nvt_tensor(pos, n, ci, off, nbr, rho):
+    """The fused kernels' NVT vote + tensor sums on the host (numpy in, (m, 6) float32 out)."""
+    import numpy as np
+    pos = np.ascontiguousarray(pos, np.float32); n = np.ascontiguousarray(n, np.float32)
+    ci = np.ascontiguousarray(ci, np.int64); off = np.ascontiguousarray(off, np.int64)
+    nbr = np.ascontiguousarray(nbr, np.int64)
+    out = np.empty((len(ci), 6), np.float32)
+    check(lib().pcd_host_nvt_tensor(pos.ctypes.data, n.ctypes.data, ci.ctypes.data, off.ctypes.data, nbr.ctypes.data,
+                                    len(ci), float(rho), out.ctypes.data), "pcd_host_nvt_tensor")
     return out
 
 

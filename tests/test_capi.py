@@ -142,3 +142,72 @@ def test_orientation_host_matches_oracle(golden):
     assert ((n.numpy() * ref).sum(1) > 0.999).mean() > 0.995
     # and with the reference's own oriented normals
     assert (np.sign((n.numpy() * lat["n17_j1_n"]).sum(1)) > 0).mean() > 0.99
+
+
+def _nvt_pairs(rng, m, k, rho):
+    """Rows of k (v_j, n_j) around v_i = 0 whose |c| sits at cos(rho) within 1e-8 .. 1e-4, plus random, parallel
+    (no vote in the row) and degenerate (|dv| tiny or zero) pairs."""
+    u = rng.standard_normal((m, k, 3)); u /= np.linalg.norm(u, axis=-1, keepdims=True)
+    p = rng.standard_normal((m, k, 3)); p -= (p * u).sum(-1, keepdims=True) * u
+    p /= np.linalg.norm(p, axis=-1, keepdims=True)
+    ct = math.cos(rho)
+    rel = rng.choice([-1e-4, -1e-5, -1e-6, -1e-7, -1e-8, 0.0, 1e-8, 1e-7, 1e-6, 1e-5, 1e-4], size=(m, k))
+    a = ct * (1 + rel) * rng.choice([-1.0, 1.0], size=(m, k))
+    scale = rng.uniform(0.9, 1.1, size=(m, k))
+    nj = scale[..., None] * (a[..., None] * u + np.sqrt(np.maximum(1 - a * a, 0))[..., None] * p)
+    length = 10.0 ** rng.uniform(-4, 2, size=(m, k))
+    dv = u * length[..., None]
+    rnd = rng.random((m, k)) < 0.2                                  # random pairs
+    nj[rnd] = rng.standard_normal((int(rnd.sum()), 3))
+    nj[m // 8:m // 4] = u[m // 8:m // 4] * rng.choice([-1.0, 1.0], size=(m // 4 - m // 8, k, 1))   # no vote
+    dv[:, 0] *= np.where(rng.random(m) < 0.1, 1e-13, 1.0)[:, None]   # below F.normalize's eps
+    dv[:, 1] *= np.where(rng.random(m) < 0.5, 0.0, 1.0)[:, None]     # zero (the row itself)
+    return dv.astype(np.float32), nj.astype(np.float32)
+
+
+def test_host_nvt_vote_and_sums_match_reference_expression():
+    """The fused kernels' squared-form vote with its exact fallback decides every pair exactly like the reference's
+    acos(|clamp(normalize(dv) . n_j)|) > rho in f32 (same libm acosf), and the tensor sums (voting rows in list
+    order, all-ones fallback) are bit-identical to a sequential f32 restatement (Decompositionor.py:278-300)."""
+    libm = ctypes.CDLL("libm.so.6")
+    libm.acosf.restype = ctypes.c_float
+    libm.acosf.argtypes = [ctypes.c_float]
+    acosf = np.vectorize(lambda x: libm.acosf(float(x)), otypes=[np.float32])
+    rng = np.random.default_rng(17)
+    m, k = 2048, 32
+    F = np.float32
+    for rho in (math.pi * 5 / 12, 0.3, math.pi / 2 + 0.01):
+        dv, nj = _nvt_pairs(rng, m, k, rho)
+        # rows 0..7: |c| at the f32 neighbours of cos(rho) (dv along an axis with power-of-two length, so the
+        # reference's normalisation is exact and c is exactly the chosen value)
+        ct = np.float32(math.cos(np.float32(rho)))
+        cs = np.array([ct + i * np.spacing(ct) for i in range(-128, 128)], F)[:8 * k]
+        for r in range(8):
+            axis = r % 3
+            L = F(2.0 ** (r - 3))
+            sel = cs[r * k:(r + 1) * k]
+            dv[r] = 0
+            dv[r, :, axis] = L * (1 if r % 2 == 0 else -1)
+            nj[r] = 0
+            nj[r, :, axis] = sel * (1 if r < 4 else -1)
+            nj[r, :, (axis + 1) % 3] = np.sqrt(np.maximum(1 - sel.astype(np.float64) ** 2, 0)).astype(F)
+        # layout: point 0 = the centre at the origin, pairs after it
+        pos = np.concatenate([np.zeros((1, 3), F), dv.reshape(-1, 3)])
+        n = np.concatenate([np.zeros((1, 3), F), nj.reshape(-1, 3)])
+        ci = np.zeros(m, np.int64)
+        off = np.arange(m + 1, dtype=np.int64) * k
+        nbr = 1 + np.arange(m * k, dtype=np.int64)
+        T = nat.host_nvt_tensor(pos, n, ci, off, nbr, rho)
+        d = pos[nbr].reshape(m, k, 3) - pos[0]
+        den = np.maximum(np.sqrt((d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]), F(1e-12))
+        dn = d / den[..., None]
+        c = np.abs(np.clip((dn[..., 0] * nj[..., 0] + dn[..., 1] * nj[..., 1]) + dn[..., 2] * nj[..., 2], -1, 1))
+        w = acosf(c) > F(rho)
+        w[w.sum(1) == 0] = True
+        acc = np.zeros((m, 6), F)
+        comps = [(0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2)]
+        for t in range(k):
+            for q, (x, y) in enumerate(comps):
+                acc[:, q] = np.where(w[:, t], acc[:, q] + nj[:, t, x] * nj[:, t, y], acc[:, q]).astype(F)
+        ref = acc / w.sum(1).astype(F)[:, None]
+        np.testing.assert_array_equal(T, ref)
