@@ -240,35 +240,60 @@ PCD_DEV unsigned long long anchor_cap(Vec3 q, float4 a) {
 
 // The anchor test for every active row; certified rows get their kstore-column list, the others go to the redo
 // list.  (NVT1 runs afterwards over all rows, k_nvt1.)
+// VALU-lean ordering: the KA candidates are ranked by 32-bit keys (fixed-point d² << 6 | list slot), so a
+// compare-exchange is one min + one max instead of a 64-bit compare and four selects; the slot -> snapshot rank
+// map sits in LDS (slot-major [KA][BS]: bank = lane for any slot, conflict-free).  Fixed point
+// floor(d² · 2^26 / R²) with R >= every candidate's distance is monotone in d², so where the first kstore + 1
+// sorted keys differ in their fixed parts the order and set are exactly those of the (d², rank) keys; any tie there
+// (an exact d² tie included, which the rank would break) sends the row to the redo search instead.  The
+// certificate counts candidates below the squared anchor bound, a rounding-safe restatement of anchor_holds.
+// Rows that fail take the exact redo path, so the stored lists are bit-identical to the 64-bit-key ordering.
+static constexpr int kAnchorBS = 128;
 template <int K, int KA>
-__global__ __launch_bounds__(256) void k_knn_anchor(GridView g, const float4* __restrict__ pos, int64_t N, RowMap rm,
-                                                     int kstore, const float4* __restrict__ anc,
-                                                     const int32_t* __restrict__ alist, int32_t* __restrict__ idx,
-                                                     uint8_t* __restrict__ fail) {
-    static_assert(KA == 2 * K, "anchor lists hold twice the list cap");
-    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const float4* __restrict__ pos, int64_t N,
+                                                          RowMap rm, int kstore, const float4* __restrict__ anc,
+                                                          const int32_t* __restrict__ alist,
+                                                          int32_t* __restrict__ idx, uint8_t* __restrict__ fail) {
+    static_assert(KA == 2 * K && KA <= 64, "anchor lists hold twice the list cap; 6 slot bits");
+    __shared__ uint32_t s_r[KA * kAnchorBS];
+    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * kAnchorBS + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 p4 = pos[i];
     const Vec3 vi = v3(p4.x, p4.y, p4.z);
     const float4 a = anc[i];
-    unsigned long long c[KA];
-    uint32_t r[KA];
+    const float delta = sqrtf(sq3(vi - v3(a.x, a.y, a.z)));
+    // anchor_holds(d²_k) <=> sqrt(d²_k)(1+e) + delta(1+e) < D(1-e); squared, with 1e-6 for the rounding of the square
+    const float rhs = a.w * (1.f - kAnchorEps) - delta * (1.f + kAnchorEps);
+    if (!(rhs > 0.f)) { fail[t0] = 1; return; }     // no anchor (NaN radius) or moved too far
+    const float bnd = rhs / (1.f + kAnchorEps);
+    const float T = bnd * bnd * (1.f - 1e-6f);
+    // every list point is within D of the anchor, hence within D + delta of q
+    const float R = (a.w + delta) * (1.f + 1e-5f);
+    const float S = 67108864.f / fmaxf(R * R, 1e-30f);
+    uint32_t r[KA], c[KA];
 #pragma unroll
     for (int t = 0; t < KA; ++t) r[t] = (uint32_t)__builtin_nontemporal_load(alist + (int64_t)t * N + i);
+    int below = 0;
 #pragma unroll
-    for (int t = 0; t < KA; ++t) c[t] = cand_key<false>(vi, g.pts[min(r[t], (uint32_t)(N - 1))], r[t]);
+    for (int t = 0; t < KA; ++t) {
+        const uint32_t rt = min(r[t], (uint32_t)(N - 1));
+        s_r[t * kAnchorBS + threadIdx.x] = rt;
+        const float d2 = dist2(vi, g.pts[rt]);
+        below += d2 < T ? 1 : 0;
+        c[t] = ((uint32_t)fminf(d2 * S, 67108863.f) << 6) | (uint32_t)t;
+    }
     bitonic_sort<KA>(c);
-    float dk = 0.f;
+    bool ok = below >= kstore;
 #pragma unroll
-    for (int t = 0; t < KA; ++t)
-        if (t == kstore - 1) dk = __uint_as_float((unsigned)(c[t] >> 32));
-    const bool ok = anchor_holds(dk, vi, a);
+    for (int t = 0; t < K; ++t)
+        if (t < kstore) ok = ok && (c[t] >> 6) < (c[t + 1] >> 6);
     fail[t0] = ok ? 0 : 1;            // -> ordered redo list (rocprim::select), so redo rows stay in spatial order
     if (!ok) return;
 #pragma unroll
     for (int t = 0; t < K; ++t)
-        if (t < kstore) __builtin_nontemporal_store((int32_t)(uint32_t)(c[t] & 0xFFFFFFFFull), idx + (int64_t)t * N + i);
+        if (t < kstore)
+            __builtin_nontemporal_store((int32_t)s_r[(c[t] & 63u) * kAnchorBS + threadIdx.x], idx + (int64_t)t * N + i);
 }
 
 // NVT1 + eigh + VU smoothing over the stored lists (lane per active row); checks every list entry and, for
@@ -595,6 +620,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     float4* P = dn->pos[dn->cur];
     const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
     const dim3 grd_wave((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), dense ? 8192 : 2048));
+    const dim3 grd_anc((unsigned)cdiv(rm.nq, kAnchorBS));
     int rc = PCD_OK;
 #define PCD_K1A(C)                                                                                                     \
     case C:                                                                                                            \
@@ -602,8 +628,8 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
             hipLaunchKernelGGL((k_knn_redo_wave<2 * C, true>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,    \
                                dn->alist, dn->idx, dn->redo, dn->redo_cnt);                                            \
         } else {                                                                                                       \
-            hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd, blk, 0, st, gv, P, N, rm, kstore, dn->anc, dn->alist,    \
-                               dn->idx, dn->fail);                                                                     \
+            hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd_anc, dim3(kAnchorBS), 0, st, gv, P, N, rm, kstore,        \
+                               dn->anc, dn->alist, dn->idx, dn->fail);                                                 \
             if ((rc = select_redo(dn, rm, st)) != PCD_OK) return rc;                                                   \
             hipLaunchKernelGGL((k_knn_redo_wave<2 * C, false>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,   \
                                dn->alist, dn->idx, dn->redo, dn->redo_cnt);                                            \

@@ -235,9 +235,16 @@ PCD_DEV void bitonic_merge(unsigned long long (&v)[TOT]) {
     }
 }
 
+// 32-bit keys without payload: a compare-exchange is one v_min_u32 + one v_max_u32.
+PCD_DEV void cswap(uint32_t& a, uint32_t& b) {
+    const uint32_t lo = min(a, b);
+    b = max(a, b);
+    a = lo;
+}
+
 // Ascending bitonic sort of v[0..N).
-template <int N>
-PCD_DEV void bitonic_sort(unsigned long long (&v)[N]) {
+template <int N, typename T>
+PCD_DEV void bitonic_sort(T (&v)[N]) {
 #pragma unroll
     for (int size = 2; size <= N; size <<= 1) {
 #pragma unroll

@@ -4,6 +4,7 @@
 mkdir -p gpurun_out
 for spec in "$@"; do
   name="${spec%%:*}"; rest="${spec#*:}"; tmo="${rest%%:*}"; cmd="${rest#*:}"
+  mkdir -p "gpurun_out/$(dirname "$name")"
   echo "== $name ($tmo s): $cmd"
   timeout -k 10 "$tmo" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
   rc=$?
