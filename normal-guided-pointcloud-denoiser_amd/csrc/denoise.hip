@@ -339,8 +339,14 @@ __global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restri
 // anchor list re-keyed here when there is one (KA distinct points: its largest key bounds the new KA-th key).
 // Writes the anchor, its list and the kstore-column kNN list.
 // DENSE: every active row (no anchors yet); else the rows on the redo list.  Grid-stride over waves.
+#ifndef PCD_REDO_OCC
+#define PCD_REDO_OCC 4
+#endif
+#ifndef PCD_REDO_GRID
+#define PCD_REDO_GRID 2048
+#endif
 template <int KA, bool DENSE>
-__global__ __launch_bounds__(256, 4) void k_knn_redo_wave(GridView g, const float4* __restrict__ pos, int64_t N, RowMap rm,
+__global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g, const float4* __restrict__ pos, int64_t N, RowMap rm,
                                                         int kstore, float4* __restrict__ anc,
                                                         int32_t* __restrict__ alist, int32_t* __restrict__ idx,
                                                         const int32_t* __restrict__ redo,
@@ -404,19 +410,46 @@ PCD_DEV void gather_rows(const float4* __restrict__ pos, const int32_t* __restri
 }
 
 // Flat-phase centre, pass 1: per-block f64 partial sums of the k_u neighbour rows of the class-c points.
+// Each thread walks rows t, t+G, t+2G, ... (G = grid threads) kRowsInFlight at a time: all their list and point loads
+// are issued together, then accumulated in the same row order as a one-row loop (bit-identical sums).
+#ifndef PCD_ROWS_IN_FLIGHT
+#define PCD_ROWS_IN_FLIGHT 2
+#endif
+static constexpr int kRowsInFlight = PCD_ROWS_IN_FLIGHT;
 template <int KU>
-__global__ void k_class_rows_sum(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N, RowMap rm,
+PCD_DEV void gather_rows_batch(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N, RowMap rm,
+                               const uint8_t* __restrict__ cls, int c, int ku, int64_t t, int64_t G,
+                               bool (&on)[kRowsInFlight], float4 (&v)[kRowsInFlight][KU]) {
+    int64_t ii[kRowsInFlight];
+#pragma unroll
+    for (int r = 0; r < kRowsInFlight; ++r) {
+        const int64_t tt = t + r * G;
+        ii[r] = tt < rm.nq ? rm(tt) : 0;
+        on[r] = tt < rm.nq;
+    }
+#pragma unroll
+    for (int r = 0; r < kRowsInFlight; ++r) on[r] = on[r] && cls[ii[r]] == c;
+#pragma unroll
+    for (int r = 0; r < kRowsInFlight; ++r) gather_rows<KU>(pos, idx, N, on[r] ? ii[r] : 0, ku, v[r]);
+}
+
+template <int KU>
+__global__ __launch_bounds__(256) void k_class_rows_sum(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N, RowMap rm,
                                  int ku, const uint8_t* __restrict__ cls, int c, RedC* __restrict__ part) {
     double sx = 0, sy = 0, sz = 0, cnt = 0;
-    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < rm.nq; t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = rm(t);
-        if (cls[i] != c) continue;
-        float4 v[KU];
-        gather_rows<KU>(pos, idx, N, i, ku, v);
+    const int64_t G = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < rm.nq; t += kRowsInFlight * G) {
+        bool on[kRowsInFlight];
+        float4 v[kRowsInFlight][KU];
+        gather_rows_batch<KU>(pos, idx, N, rm, cls, c, ku, t, G, on, v);
 #pragma unroll
-        for (int u = 0; u < KU; ++u)
-            if (u < ku) { sx += v[u].x; sy += v[u].y; sz += v[u].z; }
-        cnt += ku;
+        for (int r = 0; r < kRowsInFlight; ++r) {
+            if (!on[r]) continue;
+#pragma unroll
+            for (int u = 0; u < KU; ++u)
+                if (u < ku) { sx += v[r][u].x; sy += v[r][u].y; sz += v[r][u].z; }
+            cnt += ku;
+        }
     }
     __shared__ double s[4][256];
     s[0][threadIdx.x] = sx; s[1][threadIdx.x] = sy; s[2][threadIdx.x] = sz; s[3][threadIdx.x] = cnt;
@@ -455,21 +488,27 @@ __global__ void k_centre(const double* __restrict__ red, float* __restrict__ g) 
     }
 }
 
-// pass 4: delta = max ||v_j - centre|| over the same rows (Denoiser.py:107), atomicMax on the f32 bits.
+// pass 4: delta = max ||v_j - centre|| over the same rows (Denoiser.py:107), atomicMax on the f32 bits.  The max is
+// taken over d² and rooted once (sqrt is monotone); rows kRowsInFlight at a time as in pass 1.
 template <int KU>
-__global__ void k_class_rows_maxdist(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N,
+__global__ __launch_bounds__(256) void k_class_rows_maxdist(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N,
                                      RowMap rm, int ku, const uint8_t* __restrict__ cls, int c, float* __restrict__ g) {
     const Vec3 ctr = v3(g[0], g[1], g[2]);
-    float mx = 0.f;
-    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < rm.nq; t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = rm(t);
-        if (cls[i] != c) continue;
-        float4 v[KU];
-        gather_rows<KU>(pos, idx, N, i, ku, v);
+    float mx2 = 0.f;
+    const int64_t G = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < rm.nq; t += kRowsInFlight * G) {
+        bool on[kRowsInFlight];
+        float4 v[kRowsInFlight][KU];
+        gather_rows_batch<KU>(pos, idx, N, rm, cls, c, ku, t, G, on, v);
 #pragma unroll
-        for (int u = 0; u < KU; ++u)
-            if (u < ku) mx = fmaxf(mx, sqrtf(sq3(v3(v[u].x, v[u].y, v[u].z) - ctr)));
+        for (int r = 0; r < kRowsInFlight; ++r) {
+            if (!on[r]) continue;
+#pragma unroll
+            for (int u = 0; u < KU; ++u)
+                if (u < ku) mx2 = fmaxf(mx2, sq3(v3(v[r][u].x, v[r][u].y, v[r][u].z) - ctr));
+        }
     }
+    float mx = sqrtf(mx2);
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
     if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(g) + 3, __float_as_uint(mx));
 }
@@ -619,7 +658,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     const GridView gv = dn->g->view;
     float4* P = dn->pos[dn->cur];
     const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
-    const dim3 grd_wave((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), dense ? 8192 : 2048));
+    const dim3 grd_wave((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), dense ? 8192 : PCD_REDO_GRID));
     const dim3 grd_anc((unsigned)cdiv(rm.nq, kAnchorBS));
     int rc = PCD_OK;
 #define PCD_K1A(C)                                                                                                     \

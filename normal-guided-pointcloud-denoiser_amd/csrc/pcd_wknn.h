@@ -111,7 +111,10 @@ PCD_DEV unsigned long long wave_sort_survivors(unsigned long long* buf, int cnt,
     return top;
 }
 
-static constexpr int kCellsPerLane = 2;                 // cells per lane per chunk
+#ifndef PCD_WAVE_CPL
+#define PCD_WAVE_CPL 2
+#endif
+static constexpr int kCellsPerLane = PCD_WAVE_CPL;      // cells per lane per chunk
 static constexpr int kChunkCells = 64 * kCellsPerLane;  // cells per chunk
 static constexpr int kChunkLog2 = kCellsPerLane == 1 ? 6 : kCellsPerLane == 2 ? 7 : kCellsPerLane == 4 ? 8 : 9;
 struct WaveCells {          // per-wave LDS scratch for one chunk of cells
@@ -131,7 +134,10 @@ PCD_DEV void wave_append(bool pass, unsigned long long key, unsigned long long* 
 // brick-hash probes, then brick-block loads, are each issued together (two memory round trips for the chunk);
 // then the chunk's flattened candidate rows in rounds of kWaveRows per lane -- every row index first (binary search
 // of the count scan in LDS), then all the point loads at once, then the keys.
-static constexpr int kWaveRows = 4;
+#ifndef PCD_WAVE_ROWS
+#define PCD_WAVE_ROWS 4
+#endif
+static constexpr int kWaveRows = PCD_WAVE_ROWS;
 template <int K>
 PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int hi[3], unsigned long long& cap,
                            unsigned long long* buf, int& cnt, WaveCells* wc, int lane) {
