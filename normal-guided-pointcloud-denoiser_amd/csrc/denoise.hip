@@ -518,13 +518,22 @@ __global__ void k_copy_delta(const float* __restrict__ from, float* __restrict__
 }
 
 // K3: one Gauss-Seidel phase: active points of class c move (reading pin), other active points copy through.
+#ifndef PCD_PHASE_WIN
+#define PCD_PHASE_WIN 1
+#endif
 template <int KIND, int KU>
 __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, float4* __restrict__ pout,
                                                 const float4* __restrict__ fn, const float4* __restrict__ edge,
                                                 const int32_t* __restrict__ idx, int64_t N, RowMap rm, int ku,
                                                 const uint8_t* __restrict__ cls, int c, const float* __restrict__ g,
                                                 float d, float alpha) {
-    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    // the flat phase moves most rows: its neighbour rows come from an LDS window of pin / fn around the block
+    constexpr bool WIN = PCD_PHASE_WIN && (KIND == PCD_STEP_FLAT);
+    __shared__ float4 s_pos[WIN ? kWinRows : 1], s_fn[WIN ? kWinRows : 1];
+    const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
+    int64_t lo = 0;
+    if constexpr (WIN) lo = stage_window(pin, fn, N, rm(b0 < rm.nq ? b0 : rm.nq - 1), s_pos, s_fn);
+    const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 p4 = pin[i];
@@ -533,7 +542,10 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     const Rows4 P{pin}, F{fn};
     const ColNb nb{idx, N, i};
     Vec3 o;
-    if (KIND == PCD_STEP_FLAT) o = step_flat<KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
+    if constexpr (WIN)
+        o = step_flat<KU>(WinRows{pin, s_pos, lo}, WinRows{fn, s_fn, lo}, vi, F(i), ku, nb,
+                          __uint_as_float(((const unsigned*)g)[3]), d, alpha);
+    else if (KIND == PCD_STEP_FLAT) o = step_flat<KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
     else if (KIND == PCD_STEP_EDGE) o = step_edge<KU>(P, F, vi, Rows4{edge}(i), ku, nb, d, alpha);
     else if (KIND == PCD_STEP_FEATURE) o = step_feature<false, KU>(P, F, vi, F(i), ku, nb, 1.f, d, alpha);
     else if (KIND == PCD_STEP_NEW) o = step_feature<true, KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
