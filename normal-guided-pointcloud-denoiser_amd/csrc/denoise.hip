@@ -58,8 +58,14 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 // (one ds_read_b128) and global memory otherwise (a global load for those lanes only).  A wave's divergent 16-B
 // gathers cost the texture-address unit ~1 cycle per distinct cache line, ~35 cycles per instruction -- the
 // measured limiter of the NVT kernels (TA busy 65-77 %); LDS serves them in a few.
-static constexpr int kWinHalo = 256;                   // rows staged on either side of the block's own rows
-static constexpr int kWinRows = 256 + 2 * kWinHalo;    // rows per array in the window (12 KB each)
+// Rows staged on either side of the block's own rows, per kernel (A/B'd at 10M with tools/ab_bench.sh: NVT2 gains
+// 0.16 ms from 512, the flat phase loses 0.06 ms from it and gains 0.01 ms from 128).
+static constexpr int kWinHalo = 256;                    // NVT1
+static constexpr int kWinHaloNvt2 = 512;
+static constexpr int kWinHaloPhase = 128;
+template <int H> struct WinSize { static constexpr int rows = 256 + 2 * H; };
+static constexpr int kWinRows = WinSize<kWinHalo>::rows;
+template <int H = kWinHalo>
 struct WinRows {
     const float4* g;
     const float4* s;
@@ -67,17 +73,18 @@ struct WinRows {
     PCD_DEV Vec3 operator()(int64_t j) const {
         const uint64_t o = (uint64_t)(j - lo);
         float4 q;
-        if (o < (uint64_t)kWinRows) q = s[o];
+        if (o < (uint64_t)WinSize<H>::rows) q = s[o];
         else q = g[j];
         return v3(q.x, q.y, q.z);
     }
 };
 // Stage rows [lo, lo + kWinRows) of a and b (clipped to [0, N)) for the block whose first active row is i_first.
+template <int H = kWinHalo>
 PCD_DEV int64_t stage_window(const float4* __restrict__ a, const float4* __restrict__ b, int64_t N, int64_t i_first,
                              float4* sa, float4* sb) {
-    int64_t lo = i_first - kWinHalo;
+    int64_t lo = i_first - H;
     lo = lo < 0 ? 0 : lo;
-    for (int r = threadIdx.x; r < kWinRows; r += blockDim.x) {
+    for (int r = threadIdx.x; r < WinSize<H>::rows; r += blockDim.x) {
         const int64_t j = lo + r;
         if (j < N) { sa[r] = a[j]; sb[r] = b[j]; }
     }
@@ -326,7 +333,7 @@ __global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restri
             if (t == kstore - 1) dk = dist2(vi, g.pts[l[t]]);
         if (!cov.holds(vi, dk)) atomicOr(err, 2);
     }
-    const Sym3 T = nvt_tensor<K>(WinRows{pos, s_pos, lo}, WinRows{nrm, s_nrm, lo}, vi, k, RegNb32{l}, rho,
+    const Sym3 T = nvt_tensor<K>(WinRows<>{pos, s_pos, lo}, WinRows<>{nrm, s_nrm, lo}, vi, k, RegNb32{l}, rho,
                                  ColNbSafe{idx, N, i});
     float w[3], V[3][3];
     eigh3(T, w, V);
@@ -381,14 +388,14 @@ __global__ __launch_bounds__(256) void k_nvt2(const float4* __restrict__ pos, co
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                float rho, float scale, uint8_t* __restrict__ cls,
                                                float4* __restrict__ edge) {
-    __shared__ float4 s_pos[kWinRows], s_fn[kWinRows];
+    __shared__ float4 s_pos[WinSize<kWinHaloNvt2>::rows], s_fn[WinSize<kWinHaloNvt2>::rows];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
-    const int64_t lo = stage_window(pos, fn, N, rm(b0), s_pos, s_fn);
+    const int64_t lo = stage_window<kWinHaloNvt2>(pos, fn, N, rm(b0), s_pos, s_fn);
     const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 p4 = pos[i];
-    const Sym3 T = nvt_tensor<K>(WinRows{pos, s_pos, lo}, WinRows{fn, s_fn, lo}, v3(p4.x, p4.y, p4.z), k,
+    const Sym3 T = nvt_tensor<K>(WinRows<kWinHaloNvt2>{pos, s_pos, lo}, WinRows<kWinHaloNvt2>{fn, s_fn, lo}, v3(p4.x, p4.y, p4.z), k,
                                  ColNbStream{idx, N, i}, rho, ColNbSafe{idx, N, i});
     float w[3], V[3][3];
     eigh3(T, w, V);
@@ -529,10 +536,10 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
                                                 float d, float alpha) {
     // the flat phase moves most rows: its neighbour rows come from an LDS window of pin / fn around the block
     constexpr bool WIN = PCD_PHASE_WIN && (KIND == PCD_STEP_FLAT);
-    __shared__ float4 s_pos[WIN ? kWinRows : 1], s_fn[WIN ? kWinRows : 1];
+    __shared__ float4 s_pos[WIN ? WinSize<kWinHaloPhase>::rows : 1], s_fn[WIN ? WinSize<kWinHaloPhase>::rows : 1];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
     int64_t lo = 0;
-    if constexpr (WIN) lo = stage_window(pin, fn, N, rm(b0 < rm.nq ? b0 : rm.nq - 1), s_pos, s_fn);
+    if constexpr (WIN) lo = stage_window<kWinHaloPhase>(pin, fn, N, rm(b0 < rm.nq ? b0 : rm.nq - 1), s_pos, s_fn);
     const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
@@ -543,7 +550,7 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     const ColNb nb{idx, N, i};
     Vec3 o;
     if constexpr (WIN)
-        o = step_flat<KU>(WinRows{pin, s_pos, lo}, WinRows{fn, s_fn, lo}, vi, F(i), ku, nb,
+        o = step_flat<KU>(WinRows<kWinHaloPhase>{pin, s_pos, lo}, WinRows<kWinHaloPhase>{fn, s_fn, lo}, vi, F(i), ku, nb,
                           __uint_as_float(((const unsigned*)g)[3]), d, alpha);
     else if (KIND == PCD_STEP_FLAT) o = step_flat<KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
     else if (KIND == PCD_STEP_EDGE) o = step_edge<KU>(P, F, vi, Rows4{edge}(i), ku, nb, d, alpha);
