@@ -176,15 +176,23 @@ int pcd_denoiser_store(pcd_denoiser* dn, float* pos, float* n, int64_t* classes,
  * buffer, one sorted drain).  Results are identical either way (tested bitwise); it only changes the work done.
  * reset_seed forgets the stored list, so the next iterate() runs unseeded. */
 int pcd_denoiser_set_seeding(pcd_denoiser* dn, int enable);
+/* LDS row windows (default ON): NVT1, NVT2 and the flat phase stage a window of rows around each block's own rows
+ * in LDS and read neighbours from it when they fall inside.  OFF reads every neighbour from global memory: same
+ * results bit for bit (the parity tests check this); a diagnostic / reference switch. */
+int pcd_denoiser_set_windows(pcd_denoiser* dn, int enable);
 int pcd_denoiser_reset_seed(pcd_denoiser* dn);
 /* Anchored search (default ON, applies to seeded searches with k, k_update <= 32): each point keeps an anchor --
  * a position, the exact 2K nearest snapshot points there (K = the list cap 8/16/32) and their 2K-th distance D.
  * When the current k-th distance over that list is below D - |q - anchor|, the list's top k IS the snapshot's
- * k-NN (no grid search); the few queries that fail are re-anchored by a full grid search.  Same results (tested
- * bitwise).  Anchors depend only on the snapshot: they survive load(); reset_seed drops them. */
+ * k-NN (no grid search); the few queries that fail are re-anchored by a wave-per-query grid search (the rare
+ * query whose quantised ordering is ambiguous by the exact-key search).  Same results (tested bitwise).  Anchors depend only on the snapshot: they survive load(); reset_seed drops them. */
 int pcd_denoiser_set_anchoring(pcd_denoiser* dn, int enable);
 /* Diagnostics: rows re-anchored by the last anchored kNN stage (-1: none ran).  Synchronises `stream`. */
 int pcd_denoiser_anchor_stats(pcd_denoiser* dn, int64_t* redo_rows, void* stream);
+/* Diagnostics of the last anchored kNN stage: out4 = {rows re-anchored, of which spilled from the quantised-key
+ * search to the exact-key wave search, of those: with a cap box over 4096 cells, with an ambiguous quantised order
+ * or too few points under a dense cap}; -1 when no anchored stage ran.  Synchronises `stream`. */
+int pcd_denoiser_tile_stats(pcd_denoiser* dn, int64_t* out4, void* stream);
 /* Profiling aid: with timing enabled, every iteration (up to 256) records HIP events on its stream between the
  * stages; get_timing returns each stage's elapsed ms AVERAGED over the iterations recorded since set_timing or
  * the previous get_timing (slots: kNN+NVT1, NVT2, phase 0, phase 1, phase 2, finish, -), then starts over. */

@@ -24,7 +24,7 @@
 
 #include "pcd_knn.h"
 #include "pcd_ops.h"
-#include "pcd_wknn.h"
+#include "pcd_qknn.h"
 
 namespace pcd {
 int knn_cap(int k);
@@ -79,9 +79,13 @@ struct WinRows {
     }
 };
 // Stage rows [lo, lo + kWinRows) of a and b (clipped to [0, N)) for the block whose first active row is i_first.
+// on == 0 (pcd_denoiser_set_windows, block-uniform): nothing is staged and every row is read from global memory --
+// the reference path the windowed reads are checked against bitwise.
+static constexpr int64_t kNoWindow = -(1ll << 60);
 template <int H = kWinHalo>
 PCD_DEV int64_t stage_window(const float4* __restrict__ a, const float4* __restrict__ b, int64_t N, int64_t i_first,
-                             float4* sa, float4* sb) {
+                             float4* sa, float4* sb, int on) {
+    if (!on) return kNoWindow;
     int64_t lo = i_first - H;
     lo = lo < 0 ? 0 : lo;
     for (int r = threadIdx.x; r < WinSize<H>::rows; r += blockDim.x) {
@@ -117,13 +121,6 @@ __global__ void k_store(const float4* __restrict__ pos_s, const float4* __restri
     if (cls) cls[i] = cls_s[r];
     if (edge) { const float4 p = edge_s[r]; edge[3 * i] = p.x; edge[3 * i + 1] = p.y; edge[3 * i + 2] = p.z; }
 }
-
-// Active-row view: thread t works on row rows[t] (sorted order), or on row t when rows is null.
-struct RowMap {
-    const int32_t* rows;
-    int64_t nq;
-    PCD_DEV int64_t operator()(int64_t t) const { return rows ? (int64_t)rows[t] : t; }
-};
 
 // Local snapshot coverage: the kNN of a query is exact when its k-ball lies inside this box (spatial slabs:
 // the slab widened by the halo).  Disabled when lo > hi on axis 0.
@@ -236,15 +233,6 @@ PCD_DEV bool anchor_holds(float d2k, Vec3 q, float4 a) {
     return a.w >= 0.f && dq + delta < a.w * (1.f - kAnchorEps);
 }
 
-// Acceptance cap for re-anchoring at q: the KA anchor points are within D of a, hence within D + |q - a| of q, so
-// the KA-th key at q is below this bound (rounding margin included).  No list read: the redo rows are sparse, and
-// their column-major list rows would cost a cache line per entry.
-PCD_DEV unsigned long long anchor_cap(Vec3 q, float4 a) {
-    const float R = (a.w + sqrtf(sq3(q - v3(a.x, a.y, a.z)))) * (1.f + 1e-5f) + 1e-30f;
-    const float R2 = R * R * (1.f + 1e-5f);
-    return ((unsigned long long)__float_as_uint(R2) << 32) | 0xFFFFFFFFull;
-}
-
 // The anchor test for every active row; certified rows get their kstore-column list, the others go to the redo
 // list.  (NVT1 runs afterwards over all rows, k_nvt1.)
 // VALU-lean ordering: the KA candidates are ranked by 32-bit keys (fixed-point d² << 6 | list slot), so a
@@ -264,43 +252,52 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
     static_assert(KA == 2 * K && KA <= 64, "anchor lists hold twice the list cap; 6 slot bits");
     __shared__ uint32_t s_r[KA * kAnchorBS];
     const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * kAnchorBS + threadIdx.x;
-    if (t0 >= rm.nq) return;
-    const int64_t i = rm(t0);
-    const float4 p4 = pos[i];
-    const Vec3 vi = v3(p4.x, p4.y, p4.z);
-    const float4 a = anc[i];
-    const float delta = sqrtf(sq3(vi - v3(a.x, a.y, a.z)));
-    // anchor_holds(d²_k) <=> sqrt(d²_k)(1+e) + delta(1+e) < D(1-e); squared, with 1e-6 for the rounding of the square
-    const float rhs = a.w * (1.f - kAnchorEps) - delta * (1.f + kAnchorEps);
-    if (!(rhs > 0.f)) { fail[t0] = 1; return; }     // no anchor (NaN radius) or moved too far
-    const float bnd = rhs / (1.f + kAnchorEps);
-    const float T = bnd * bnd * (1.f - 1e-6f);
-    // every list point is within D of the anchor, hence within D + delta of q
-    const float R = (a.w + delta) * (1.f + 1e-5f);
-    const float S = 67108864.f / fmaxf(R * R, 1e-30f);
-    uint32_t r[KA], c[KA];
+    bool failed = false;
+    if (t0 < rm.nq) {
+        const int64_t i = rm(t0);
+        const float4 p4 = pos[i];
+        const Vec3 vi = v3(p4.x, p4.y, p4.z);
+        const float4 a = anc[i];
+        const float delta = sqrtf(sq3(vi - v3(a.x, a.y, a.z)));
+        // anchor_holds(d²_k) <=> sqrt(d²_k)(1+e) + delta(1+e) < D(1-e); squared, with 1e-6 for the rounding of the square
+        const float rhs = a.w * (1.f - kAnchorEps) - delta * (1.f + kAnchorEps);
+        if (!(rhs > 0.f)) {
+            failed = true;                            // no anchor (NaN radius) or moved too far
+        } else {
+            const float bnd = rhs / (1.f + kAnchorEps);
+            const float T = bnd * bnd * (1.f - 1e-6f);
+            // every list point is within D of the anchor, hence within D + delta of q
+            const float R = (a.w + delta) * (1.f + 1e-5f);
+            const float S = 67108864.f / fmaxf(R * R, 1e-30f);
+            uint32_t r[KA], c[KA];
 #pragma unroll
-    for (int t = 0; t < KA; ++t) r[t] = (uint32_t)__builtin_nontemporal_load(alist + (int64_t)t * N + i);
-    int below = 0;
+            for (int t = 0; t < KA; ++t) r[t] = (uint32_t)__builtin_nontemporal_load(alist + (int64_t)t * N + i);
+            int below = 0;
 #pragma unroll
-    for (int t = 0; t < KA; ++t) {
-        const uint32_t rt = min(r[t], (uint32_t)(N - 1));
-        s_r[t * kAnchorBS + threadIdx.x] = rt;
-        const float d2 = dist2(vi, g.pts[rt]);
-        below += d2 < T ? 1 : 0;
-        c[t] = ((uint32_t)fminf(d2 * S, 67108863.f) << 6) | (uint32_t)t;
+            for (int t = 0; t < KA; ++t) {
+                const uint32_t rt = min(r[t], (uint32_t)(N - 1));
+                s_r[t * kAnchorBS + threadIdx.x] = rt;
+                const float d2 = dist2(vi, g.pts[rt]);
+                below += d2 < T ? 1 : 0;
+                c[t] = ((uint32_t)fminf(d2 * S, 67108863.f) << 6) | (uint32_t)t;
+            }
+            bitonic_sort<KA>(c);
+            bool ok = below >= kstore;
+#pragma unroll
+            for (int t = 0; t < K; ++t)
+                if (t < kstore) ok = ok && (c[t] >> 6) < (c[t + 1] >> 6);
+            failed = !ok;
+            if (ok) {
+#pragma unroll
+                for (int t = 0; t < K; ++t)
+                    if (t < kstore)
+                        __builtin_nontemporal_store((int32_t)s_r[(c[t] & 63u) * kAnchorBS + threadIdx.x],
+                                                    idx + (int64_t)t * N + i);
+            }
+        }
     }
-    bitonic_sort<KA>(c);
-    bool ok = below >= kstore;
-#pragma unroll
-    for (int t = 0; t < K; ++t)
-        if (t < kstore) ok = ok && (c[t] >> 6) < (c[t + 1] >> 6);
-    fail[t0] = ok ? 0 : 1;            // -> ordered redo list (rocprim::select), so redo rows stay in spatial order
-    if (!ok) return;
-#pragma unroll
-    for (int t = 0; t < K; ++t)
-        if (t < kstore)
-            __builtin_nontemporal_store((int32_t)s_r[(c[t] & 63u) * kAnchorBS + threadIdx.x], idx + (int64_t)t * N + i);
+    if (t0 < rm.nq) fail[t0] = failed ? 1 : 0;   // -> ordered redo list (rocprim::select): redo rows stay in
+                                                 // spatial order, so the waves in flight on an XCD share its L2
 }
 
 // NVT1 + eigh + VU smoothing over the stored lists (lane per active row); checks every list entry and, for
@@ -309,10 +306,10 @@ template <int K>
 __global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                int kstore, float rho, float tau, float damp, Cover cov,
-                                               float4* __restrict__ fn, int* __restrict__ err) {
+                                               float4* __restrict__ fn, int* __restrict__ err, int win) {
     __shared__ float4 s_pos[kWinRows], s_nrm[kWinRows];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
-    const int64_t lo = stage_window(pos, nrm, N, rm(b0), s_pos, s_nrm);
+    const int64_t lo = stage_window(pos, nrm, N, rm(b0), s_pos, s_nrm, win);
     const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
@@ -357,7 +354,7 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
                                                         int kstore, float4* __restrict__ anc,
                                                         int32_t* __restrict__ alist, int32_t* __restrict__ idx,
                                                         const int32_t* __restrict__ redo,
-                                                        const unsigned* __restrict__ redo_cnt) {
+                                                        const unsigned* __restrict__ redo_cnt, int* __restrict__ err) {
     __shared__ unsigned long long s_buf[4][kWaveSurv];
     __shared__ WaveCells s_cells[4];
     const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
@@ -374,11 +371,18 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
             if (a.w >= 0.f) cap = anchor_cap(q, a);
         }
         const unsigned long long top = wave_knn<KA>(g, q, cap, s_buf[wv], &s_cells[wv], lane);
-        const int32_t r = (int32_t)(uint32_t)(top & 0xFFFFFFFFull);
+        // a slot without a finite candidate (non-finite query, fewer than KA points) is never stored as an index:
+        // the row itself stands in, the error word reports it, and the anchor is dropped (NaN radius)
+        const uint32_t r32 = (uint32_t)(top & 0xFFFFFFFFull);
+        const bool valid = (uint32_t)(top >> 32) < 0x7F800000u && r32 < (uint64_t)N;
+        const int32_t r = valid ? (int32_t)r32 : (int32_t)i;
+        const bool all_valid = !__any(lane < KA && !valid);
+        if (!all_valid && lane == 0) atomicOr(err, 1);
         if (lane < KA) alist[(int64_t)lane * N + i] = r;
         if (lane < kstore) idx[(int64_t)lane * N + i] = r;
         // D: the KA-th distance (every other snapshot point is at least this far from the anchor)
-        if (lane == KA - 1) anc[i] = make_float4(q.x, q.y, q.z, sqrtf(__uint_as_float((unsigned)(top >> 32))));
+        if (lane == KA - 1)
+            anc[i] = make_float4(q.x, q.y, q.z, all_valid ? sqrtf(__uint_as_float((unsigned)(top >> 32))) : __int_as_float(0x7FC00000));
     }
 }
 
@@ -387,20 +391,28 @@ template <int K>
 __global__ __launch_bounds__(256) void k_nvt2(const float4* __restrict__ pos, const float4* __restrict__ fn,
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                float rho, float scale, uint8_t* __restrict__ cls,
-                                               float4* __restrict__ edge) {
+                                               float4* __restrict__ edge, int win) {
     __shared__ float4 s_pos[WinSize<kWinHaloNvt2>::rows], s_fn[WinSize<kWinHaloNvt2>::rows];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
-    const int64_t lo = stage_window<kWinHaloNvt2>(pos, fn, N, rm(b0), s_pos, s_fn);
+    const int64_t lo = stage_window<kWinHaloNvt2>(pos, fn, N, rm(b0), s_pos, s_fn, win);
     const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 p4 = pos[i];
     const Sym3 T = nvt_tensor<K>(WinRows<kWinHaloNvt2>{pos, s_pos, lo}, WinRows<kWinHaloNvt2>{fn, s_fn, lo}, v3(p4.x, p4.y, p4.z), k,
                                  ColNbStream{idx, N, i}, rho, ColNbSafe{idx, N, i});
+#ifdef PCD_NVT2_LAPACK
     float w[3], V[3][3];
     eigh3(T, w, V);
     cls[i] = (uint8_t)classify(w, scale, nullptr);
     store4(edge, i, v3(V[0][0], V[1][0], V[2][0]));
+#else
+    float w[3];
+    Vec3 y;
+    eigh3_min(T, w, y);
+    cls[i] = (uint8_t)classify(w, scale, nullptr);
+    store4(edge, i, y);
+#endif
 }
 
 struct RedC { double sx, sy, sz, cnt; };
@@ -533,13 +545,13 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
                                                 const float4* __restrict__ fn, const float4* __restrict__ edge,
                                                 const int32_t* __restrict__ idx, int64_t N, RowMap rm, int ku,
                                                 const uint8_t* __restrict__ cls, int c, const float* __restrict__ g,
-                                                float d, float alpha) {
+                                                float d, float alpha, int win) {
     // the flat phase moves most rows: its neighbour rows come from an LDS window of pin / fn around the block
     constexpr bool WIN = PCD_PHASE_WIN && (KIND == PCD_STEP_FLAT);
     __shared__ float4 s_pos[WIN ? WinSize<kWinHaloPhase>::rows : 1], s_fn[WIN ? WinSize<kWinHaloPhase>::rows : 1];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
     int64_t lo = 0;
-    if constexpr (WIN) lo = stage_window<kWinHaloPhase>(pin, fn, N, rm(b0 < rm.nq ? b0 : rm.nq - 1), s_pos, s_fn);
+    if constexpr (WIN) lo = stage_window<kWinHaloPhase>(pin, fn, N, rm(b0 < rm.nq ? b0 : rm.nq - 1), s_pos, s_fn, win);
     const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
@@ -595,14 +607,16 @@ struct pcd_denoiser {
     // anchored kNN (list cap <= 32): anchors + their 2K-lists, the redo list of queries that failed the test
     float4* anc = nullptr;
     int32_t* alist = nullptr;
-    int32_t* redo = nullptr;
-    unsigned* redo_cnt = nullptr;
+    int32_t* redo = nullptr;      // rows that failed the anchor test (redo list)
+    int32_t* spill = nullptr;     // rows the re-anchoring search hands to the exact-key wave search
+    RqStats* rqs = nullptr;       // lengths of the redo and spill lists (pcd_qknn.h)
     uint8_t* fail = nullptr;      // per active row: anchor test failed
     void* sel_tmp = nullptr;      // rocprim::select scratch
     size_t sel_bytes = 0;
     int anchor_ka = 0;            // KA of the stored anchors (0: none)
     int64_t last_dense = -1;      // rows of the last anchored stage when it re-anchored every row, else -1
     bool anchoring = true;        // anchored kNN for seeded searches (pcd_denoiser_set_anchoring)
+    int windows = 1;              // LDS row windows in NVT1 / NVT2 / the flat phase (pcd_denoiser_set_windows)
     bool loaded = false, iterated = false;
     bool timing = false;
     std::vector<hipEvent_t> ev;   // kTimingSets sets of kTimingEvents events, one set per timed iteration
@@ -636,13 +650,13 @@ static bool phase_is_global(const pcd_denoise_params* p, int ph) {
     return p->phase_kind[ph] == PCD_STEP_FLAT || p->phase_kind[ph] == PCD_STEP_NEW;
 }
 
-// rows whose anchor test failed (fail[t] != 0), in row order -> dn->redo[0 .. *dn->redo_cnt)
-static int select_redo(pcd_denoiser* dn, const RowMap& rm, hipStream_t st) {
+// rows whose anchor test failed (fail[t] != 0), in row order -> list[0 .. *cnt)
+static int select_rows(pcd_denoiser* dn, const RowMap& rm, int32_t* list, unsigned* cnt, hipStream_t st) {
     const size_t n = (size_t)rm.nq;
     size_t bytes = 0;
     rocprim::counting_iterator<int32_t> ids(0);
-    if (rm.rows) (void)rocprim::select(nullptr, bytes, rm.rows, dn->fail, dn->redo, dn->redo_cnt, n, st);
-    else (void)rocprim::select(nullptr, bytes, ids, dn->fail, dn->redo, dn->redo_cnt, n, st);
+    if (rm.rows) (void)rocprim::select(nullptr, bytes, rm.rows, dn->fail, list, cnt, n, st);
+    else (void)rocprim::select(nullptr, bytes, ids, dn->fail, list, cnt, n, st);
     if (bytes > dn->sel_bytes) {
         (void)hipFree(dn->sel_tmp);
         dn->sel_tmp = nullptr;
@@ -650,14 +664,21 @@ static int select_redo(pcd_denoiser* dn, const RowMap& rm, hipStream_t st) {
         if (hipMalloc(&dn->sel_tmp, bytes) != hipSuccess) return fail(PCD_ERR_OOM, "pcd_denoiser: select temp");
         dn->sel_bytes = bytes;
     }
-    hipError_t e = rm.rows ? rocprim::select(dn->sel_tmp, bytes, rm.rows, dn->fail, dn->redo, dn->redo_cnt, n, st)
-                           : rocprim::select(dn->sel_tmp, bytes, ids, dn->fail, dn->redo, dn->redo_cnt, n, st);
+    hipError_t e = rm.rows ? rocprim::select(dn->sel_tmp, bytes, rm.rows, dn->fail, list, cnt, n, st)
+                           : rocprim::select(dn->sel_tmp, bytes, ids, dn->fail, list, cnt, n, st);
     if (e != hipSuccess) return fail(PCD_ERR_HIP, std::string("rocprim::select: ") + hipGetErrorString(e));
     return PCD_OK;
 }
 
-// Anchored K1 (seeded, list cap K <= 32, KA = 2K): the anchor test for every active row, then a re-anchoring
-// grid search for the rows that failed it -- or for every row when there are no anchors (of this KA) yet.
+// Anchored K1 (seeded, list cap K <= 32, KA = 2K): the anchor test for every active row, then the re-anchoring
+// search (pcd_qknn.h) of the rows that failed it -- or of every row when there are no anchors (of this KA) yet --
+// and the exact-key wave search (pcd_wknn.h) for the few rows it spills.
+#ifndef PCD_RQ_RDENSE
+#define PCD_RQ_RDENSE 1.45f
+#endif
+#ifndef PCD_RQ_GRID
+#define PCD_RQ_GRID 4096
+#endif
 static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int K, hipStream_t st) {
     const int64_t N = dn->n;
     const RowMap rm = dn->rowmap();
@@ -666,34 +687,41 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     if (!dn->anc) {
         if (hipMalloc(&dn->anc, N * sizeof(float4)) != hipSuccess ||
             hipMalloc(&dn->alist, (int64_t)2 * knn_cap(dn->kcap) * N * sizeof(int32_t)) != hipSuccess ||
-            hipMalloc(&dn->redo, N * sizeof(int32_t)) != hipSuccess || hipMalloc(&dn->fail, N) != hipSuccess ||
-            hipMalloc(&dn->redo_cnt, sizeof(unsigned)) != hipSuccess)
+            hipMalloc(&dn->redo, N * sizeof(int32_t)) != hipSuccess ||
+            hipMalloc(&dn->spill, N * sizeof(int32_t)) != hipSuccess || hipMalloc(&dn->fail, N) != hipSuccess ||
+            hipMalloc(&dn->rqs, sizeof(RqStats)) != hipSuccess)
             return fail(PCD_ERR_OOM, "pcd_denoiser: anchor buffers");
         dn->anchor_ka = 0;
     }
     const bool dense = dn->anchor_ka != KA;
     dn->last_dense = dense ? rm.nq : -1;
     if (dense) PCD_HIP(hipMemsetAsync(dn->anc, 0xFF, N * sizeof(float4), st));   // NaN radius: no anchor
+    PCD_HIP(hipMemsetAsync(dn->rqs, 0, sizeof(RqStats), st));
     const GridView gv = dn->g->view;
     float4* P = dn->pos[dn->cur];
+    unsigned* redo_cnt = &dn->rqs->redo_cnt;
+    unsigned* spill_cnt = &dn->rqs->spill_cnt;
     const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
-    const dim3 grd_wave((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), dense ? 8192 : PCD_REDO_GRID));
+    const dim3 grd_rq((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), dense ? 16384 : PCD_RQ_GRID));
+    const dim3 grd_wave((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), PCD_REDO_GRID));
     const dim3 grd_anc((unsigned)cdiv(rm.nq, kAnchorBS));
     int rc = PCD_OK;
 #define PCD_K1A(C)                                                                                                     \
     case C:                                                                                                            \
         if (dense) {                                                                                                   \
-            hipLaunchKernelGGL((k_knn_redo_wave<2 * C, true>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,    \
-                               dn->alist, dn->idx, dn->redo, dn->redo_cnt);                                            \
+            hipLaunchKernelGGL((k_knn_requery<2 * C, true>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, PCD_RQ_RDENSE,   \
+                               dn->anc, dn->alist, dn->idx, dn->redo, redo_cnt, dn->spill, spill_cnt);                 \
         } else {                                                                                                       \
             hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd_anc, dim3(kAnchorBS), 0, st, gv, P, N, rm, kstore,        \
                                dn->anc, dn->alist, dn->idx, dn->fail);                                                 \
-            if ((rc = select_redo(dn, rm, st)) != PCD_OK) return rc;                                                   \
-            hipLaunchKernelGGL((k_knn_redo_wave<2 * C, false>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,   \
-                               dn->alist, dn->idx, dn->redo, dn->redo_cnt);                                            \
+            if ((rc = select_rows(dn, rm, dn->redo, redo_cnt, st)) != PCD_OK) return rc;                               \
+            hipLaunchKernelGGL((k_knn_requery<2 * C, false>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, 0.f, dn->anc,  \
+                               dn->alist, dn->idx, dn->redo, redo_cnt, dn->spill, spill_cnt);                         \
         }                                                                                                              \
+        hipLaunchKernelGGL((k_knn_redo_wave<2 * C, false>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,       \
+                           dn->alist, dn->idx, dn->spill, spill_cnt, dn->err);                                         \
         hipLaunchKernelGGL((k_nvt1<C>), grd, blk, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore, p->rho, p->tau, \
-                           p->damp, dn->cov, dn->fn, dn->err);                                                         \
+                           p->damp, dn->cov, dn->fn, dn->err, dn->windows);                                          \
         break;
     switch (K) {
         PCD_K1A(8) PCD_K1A(16) PCD_K1A(32)
@@ -739,7 +767,7 @@ static int stage_k2(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t s
     const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
     float4* P = dn->pos[dn->cur];
 #define PCD_K2(C) \
-    case C: hipLaunchKernelGGL(k_nvt2<C>, grd, blk, 0, st, P, dn->fn, dn->idx, dn->n, rm, p->k, p->rho, p->class_scale, dn->cls, dn->edge); break;
+    case C: hipLaunchKernelGGL(k_nvt2<C>, grd, blk, 0, st, P, dn->fn, dn->idx, dn->n, rm, p->k, p->rho, p->class_scale, dn->cls, dn->edge, dn->windows); break;
     switch (list_cap(p)) {
         PCD_K2(8) PCD_K2(16) PCD_K2(32) PCD_K2(64)
         default: return fail(PCD_ERR_ARG, "unsupported k");
@@ -799,7 +827,7 @@ static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, co
     float4* pout = dn->pos[dn->cur ^ 1];
     if (rm.nq > 0) {
         const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
-#define PCD_PH2(KD, C) hipLaunchKernelGGL((k_phase<KD, C>), grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, dn->n, rm, p->k_update, dn->cls, c, gs, p->d, a)
+#define PCD_PH2(KD, C) hipLaunchKernelGGL((k_phase<KD, C>), grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, dn->n, rm, p->k_update, dn->cls, c, gs, p->d, a, dn->windows)
 #define PCD_PH(KD)                                                                                                     \
     switch (knn_cap(p->k_update)) {                                                                                    \
         case 8: PCD_PH2(KD, 8); break;                                                                                 \
@@ -874,8 +902,8 @@ int pcd_denoiser_destroy(pcd_denoiser* dn) {
     (void)hipFree(dn->pos[0]); (void)hipFree(dn->pos[1]); (void)hipFree(dn->nrm); (void)hipFree(dn->fn);
     (void)hipFree(dn->edge); (void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part);
     (void)hipFree(dn->red); (void)hipFree(dn->gscal); (void)hipFree(dn->err);
-    (void)hipFree(dn->anc); (void)hipFree(dn->alist); (void)hipFree(dn->redo); (void)hipFree(dn->redo_cnt);
-    (void)hipFree(dn->fail); (void)hipFree(dn->sel_tmp);
+    (void)hipFree(dn->anc); (void)hipFree(dn->alist); (void)hipFree(dn->redo); (void)hipFree(dn->spill);
+    (void)hipFree(dn->rqs); (void)hipFree(dn->fail); (void)hipFree(dn->sel_tmp);
     for (auto e : dn->ev) (void)hipEventDestroy(e);
     delete dn;
     return PCD_OK;
@@ -991,19 +1019,35 @@ int pcd_debug_wstats(unsigned long long* out8, int reset) {
 
 int pcd_denoiser_anchor_stats(pcd_denoiser* dn, int64_t* redo_rows, void* stream) {
     PCD_CHECK_ARG(dn && redo_rows, "null argument");
-    *redo_rows = -1;
-    if (!dn->redo_cnt || dn->anchor_ka == 0) return PCD_OK;
-    if (dn->last_dense >= 0) { *redo_rows = dn->last_dense; return PCD_OK; }
-    unsigned c = 0;
-    PCD_HIP(hipMemcpyAsync(&c, dn->redo_cnt, sizeof(unsigned), hipMemcpyDeviceToHost, as_stream(stream)));
+    int64_t v[4];
+    const int rc = pcd_denoiser_tile_stats(dn, v, stream);
+    *redo_rows = v[0];
+    return rc;
+}
+
+int pcd_denoiser_tile_stats(pcd_denoiser* dn, int64_t* out4, void* stream) {
+    PCD_CHECK_ARG(dn && out4, "null argument");
+    for (int a = 0; a < 4; ++a) out4[a] = -1;
+    if (!dn->rqs || dn->anchor_ka == 0) return PCD_OK;
+    RqStats rs;
+    PCD_HIP(hipMemcpyAsync(&rs, dn->rqs, sizeof rs, hipMemcpyDeviceToHost, as_stream(stream)));
     PCD_HIP(hipStreamSynchronize(as_stream(stream)));
-    *redo_rows = c;
+    out4[0] = dn->last_dense >= 0 ? dn->last_dense : (int64_t)rs.redo_cnt;
+    out4[1] = (int64_t)rs.spill_cnt;
+    out4[2] = (int64_t)rs.spill_big;
+    out4[3] = (int64_t)rs.spill_amb;
     return PCD_OK;
 }
 
 int pcd_denoiser_set_anchoring(pcd_denoiser* dn, int enable) {
     PCD_CHECK_ARG(dn != nullptr, "null denoiser");
     dn->anchoring = enable != 0;
+    return PCD_OK;
+}
+
+int pcd_denoiser_set_windows(pcd_denoiser* dn, int enable) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    dn->windows = enable != 0;
     return PCD_OK;
 }
 

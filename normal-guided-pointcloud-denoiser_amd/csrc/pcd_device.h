@@ -53,6 +53,13 @@ PCD_DEV int64_t xcd_block(int64_t b, int64_t nb) {
     return base + w;
 }
 
+// Active-row view: thread t works on row rows[t] (sorted order), or on row t when rows is null.
+struct RowMap {
+    const int32_t* rows;
+    int64_t nq;
+    PCD_DEV int64_t operator()(int64_t t) const { return rows ? (int64_t)rows[t] : t; }
+};
+
 // ---------------------------------------------------------------- symmetric 3x3 eigen-decomposition
 // A restatement of what torch.linalg.eigh does on the reference's CPU path for one 3x3 fp32 matrix: LAPACK ssyevd
 // (JOBZ='V', UPLO='L') = ssytd2 Householder tridiagonalisation, ssteqr implicit QL/QR with Wilkinson shifts
@@ -577,6 +584,59 @@ PCD_DEV Vec3 vu_smooth(const float w[3], const float V[3][3], Vec3 n, float tau,
     const Vec3 nn = v3(damp * n.x + acc[0], damp * n.y + acc[1], damp * n.z + acc[2]);
     const float len = sqrtf(sq3(nn));
     return v3(nn.x / len, nn.y / len, nn.z / len);
+}
+
+// ---------------------------------------------------------------- NVT2: eigenvalues + smallest eigenvector
+// NVT2's outputs are the classes (eigenvalues only) and the edge vector (the smallest eigenvalue's eigenvector,
+// used only through y·yᵀ and (x·y)·y in edge_step, Denoiser.py:53-88 -- sign-invariant).  Unlike NVT1's VU smoothing
+// (Eᵀ·M·E, Decompositionor.py:101-105), nothing here depends on LAPACK's eigenvector signs or degenerate bases, so
+// a cyclic Jacobi solve replaces the ssytd2 + ssteqr port: 4 fixed sweeps of the 3 plane rotations (fp32 Jacobi
+// converges quadratically; after 4 sweeps the off-diagonal is at rounding level), no data-dependent loop, no
+// divergence.  Eigenvalue error ~1e-7 of the trace (the tests' bound for eigenvalues is 2e-6).
+template <int P, int Q, int R>
+PCD_DEV void jacobi_rot(float (&a)[3][3], float (&V)[3][3]) {
+    const float apq = a[P][Q];
+    const float theta = (a[Q][Q] - a[P][P]) / (2.f * apq);
+    float t = 1.f / (fabsf(theta) + sqrtf(theta * theta + 1.f));
+    t = theta < 0.f ? -t : t;
+    t = apq == 0.f ? 0.f : t;                      // nothing to rotate (theta would be +-inf or NaN)
+    const float c = 1.f / sqrtf(t * t + 1.f), s = t * c;
+    a[P][P] = a[P][P] - t * apq;
+    a[Q][Q] = a[Q][Q] + t * apq;
+    a[P][Q] = a[Q][P] = 0.f;
+    const float arp = a[R][P], arq = a[R][Q];
+    a[R][P] = a[P][R] = c * arp - s * arq;
+    a[R][Q] = a[Q][R] = s * arp + c * arq;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float vp = V[i][P], vq = V[i][Q];
+        V[i][P] = c * vp - s * vq;
+        V[i][Q] = s * vp + c * vq;
+    }
+}
+// Ascending eigenvalues w of T and the eigenvector y of w[0] (unit length, arbitrary sign).
+PCD_DEV void eigh3_min(const Sym3& T, float w[3], Vec3& y) {
+    float a[3][3] = {{T.a00, T.a01, T.a02}, {T.a01, T.a11, T.a12}, {T.a02, T.a12, T.a22}};
+    float V[3][3] = {{1.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, {0.f, 0.f, 1.f}};
+#pragma unroll
+    for (int sweep = 0; sweep < 4; ++sweep) {
+        jacobi_rot<0, 1, 2>(a, V);
+        jacobi_rot<0, 2, 1>(a, V);
+        jacobi_rot<1, 2, 0>(a, V);
+    }
+    const float d0 = a[0][0], d1 = a[1][1], d2 = a[2][2];
+    // ascending order (3 compare-exchanges on (value, column)); the smallest picks its column of V
+    float e[3] = {d0, d1, d2};
+    int c[3] = {0, 1, 2};
+    auto cx = [&](int i, int j) {
+        const bool sw = e[j] < e[i];
+        const float ev = sw ? e[j] : e[i]; e[j] = sw ? e[i] : e[j]; e[i] = ev;
+        const int cv = sw ? c[j] : c[i]; c[j] = sw ? c[i] : c[j]; c[i] = cv;
+    };
+    cx(0, 1); cx(1, 2); cx(0, 1);
+    w[0] = e[0]; w[1] = e[1]; w[2] = e[2];
+    y = c[0] == 0 ? v3(V[0][0], V[1][0], V[2][0]) : c[0] == 1 ? v3(V[0][1], V[1][1], V[2][1]) : v3(V[0][2], V[1][2], V[2][2]);
+    if (!(d0 == d0 && d1 == d1 && d2 == d2)) { w[0] = w[1] = w[2] = NAN; }
 }
 
 // Decomposition.getNVTFeatures + getClasses(scale)  (Decompositionor.py:57-69)

@@ -76,7 +76,9 @@ _SIGS = {
     "pcd_denoiser_reset_seed": (c_int, [c_void_p]),
     "pcd_denoiser_set_seeding": (c_int, [c_void_p, c_int]),
     "pcd_denoiser_set_anchoring": (c_int, [c_void_p, c_int]),
+    "pcd_denoiser_set_windows": (c_int, [c_void_p, c_int]),
     "pcd_denoiser_anchor_stats": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "pcd_denoiser_tile_stats": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_denoiser_check": (c_int, [c_void_p, c_void_p]),
     "pcd_denoiser_set_rows": (c_int, [c_void_p, c_void_p, c_int64]),
     "pcd_denoiser_set_coverage": (c_int, [c_void_p, c_void_p, c_void_p]),
@@ -276,12 +278,21 @@ class FusedDenoiser:
     def set_anchoring(self, enable=True):
         check(lib().pcd_denoiser_set_anchoring(self.handle, int(bool(enable))), "pcd_denoiser_set_anchoring")
 
+    def set_windows(self, enable=True):
+        check(lib().pcd_denoiser_set_windows(self.handle, int(bool(enable))), "pcd_denoiser_set_windows")
+
     def redo_rows(self) -> int:
         """Rows re-anchored by the last anchored kNN stage (-1: none ran)."""
         v = ctypes.c_int64(0)
         check(lib().pcd_denoiser_anchor_stats(self.handle, ctypes.byref(v), c_void_p(stream_ptr())),
               "pcd_denoiser_anchor_stats")
         return v.value
+
+    def tile_stats(self) -> dict:
+        """Counters of the last anchored kNN stage (pcd_denoiser_tile_stats)."""
+        v = (ctypes.c_int64 * 4)()
+        check(lib().pcd_denoiser_tile_stats(self.handle, v, c_void_p(stream_ptr())), "pcd_denoiser_tile_stats")
+        return {"rows": v[0], "spilled": v[1], "spilled_big_box": v[2], "spilled_ambiguous": v[3]}
 
     def reset_seed(self):
         check(lib().pcd_denoiser_reset_seed(self.handle), "pcd_denoiser_reset_seed")
@@ -293,9 +304,17 @@ class FusedDenoiser:
         check(lib().pcd_denoiser_check(self.handle, c_void_p(stream_ptr())), "pcd_denoiser_check")
 
     # ---- spatial slabs: active rows, coverage, staged iteration, halo pack/unpack (include/pcd.h)
+    @staticmethod
+    def _rows_i32(rows: torch.Tensor) -> torch.Tensor:
+        """Row lists go to the C-ABI as int32_t*: any integer tensor is converted on the HIP device (the converted
+        tensor must be kept alive by the caller until the launch has consumed it)."""
+        assert not rows.is_floating_point() and not rows.is_complex(), "row indices must be an integer tensor"
+        return on_device(rows.reshape(-1), torch.int32)
+
     def set_rows(self, rows):
-        """rows: int32 device tensor of spatial-order rows (kept alive here), or None for all rows."""
-        self._rows = None if rows is None else rows.contiguous()
+        """rows: integer tensor of spatial-order rows (converted to int32 on the device and kept alive here), or
+        None for all rows."""
+        self._rows = None if rows is None else self._rows_i32(rows)
         n = 0 if rows is None else self._rows.numel()
         check(lib().pcd_denoiser_set_rows(self.handle, ptr(self._rows), n), "pcd_denoiser_set_rows")
 
@@ -312,16 +331,19 @@ class FusedDenoiser:
                                        c_void_p(stream_ptr())), "pcd_denoiser_stage")
 
     def pack(self, field: int, rows: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+        rows = self._rows_i32(rows)
         n = rows.numel()
         if out is None:
             out = torch.empty((n, 4), dtype=torch.float32, device=rows.device)
+        assert out.dtype == torch.float32 and out.is_contiguous() and out.shape == (n, 4) and out.device == rows.device
         check(lib().pcd_denoiser_pack(self.handle, int(field), ptr(rows), n, ptr(out), c_void_p(stream_ptr())),
               "pcd_denoiser_pack")
         return out
 
     def unpack(self, field: int, rows: torch.Tensor, data: torch.Tensor):
+        rows = self._rows_i32(rows)
         data = data.contiguous()
-        assert data.dtype == torch.float32 and data.shape == (rows.numel(), 4)
+        assert data.dtype == torch.float32 and data.shape == (rows.numel(), 4) and data.device == rows.device
         check(lib().pcd_denoiser_unpack(self.handle, int(field), ptr(rows), rows.numel(), ptr(data),
                                         c_void_p(stream_ptr())), "pcd_denoiser_unpack")
 

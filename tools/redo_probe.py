@@ -37,6 +37,10 @@ def main():
             q = max(st[0], 1)
             extra = (f"  | wave: q {st[0]} chunks/q {st[1] / q:.2f} rows/q {st[2] / q:.0f} reduces/q {st[3] / q:.2f} "
                      f"surv/q {st[4] / q:.0f} >128 {st[5] / q:.2f} boxcells/q {st[6] / q:.1f}")
+        if hasattr(fused, "tile_stats"):
+            ts = fused.tile_stats()
+            extra += (f"  | spilled to the exact wave search {ts['spilled']} (big box {ts['spilled_big_box']}, "
+                      f"ambiguous {ts['spilled_ambiguous']})")
         print(f"it {it:3d}: redo {r:9d} ({r / n * 100:5.2f} %)  K1 {t[0]:7.3f} ms  iteration {sum(t):7.3f} ms{extra}",
               flush=True)
 
