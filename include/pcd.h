@@ -160,6 +160,12 @@ typedef struct {
     int phase_class[3];  /* 0 flat, 1 edge, 2 corner                                                     */
     int phase_kind[3];   /* PCD_STEP_*                                                                   */
     float phase_alpha[3];
+    int jacobi;          /* 0: Gauss-Seidel across the phases (Processor.denoise, Processor.py:127-138); 1: every phase
+                            reads the iteration's input positions (Jacobi across classes: temp_pos, the thesis driver
+                            "Ours", PostProcessing.ipynb:1069-1090)                                          */
+    float clamp_global;  /* > 0: a moved point keeps its new position only while it lies within clamp_global of its
+                            position at pcd_denoiser_load, else it keeps the previous iteration's position
+                            (PostProcessing.ipynb:1088-1089, mask = ||temp_pos - original_pos|| < d); 0: off */
 } pcd_denoise_params;
 
 int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out);

@@ -105,6 +105,32 @@ class Processor:
         phases = ((0, _nat.STEP_FLAT, alphas[0]), (1, _nat.STEP_EDGE, alphas[1]), (2, _nat.STEP_FEATURE, alphas[2]))
         self._run_fused(iterations, k, k_update, d, phases, angle)
 
+    def thesisDenoise(self, iterations: int = 2, alphas=DEFAULT_ALPHAS, d: float = None,
+                      step_clamp_factor: float = 20000.0, k: int = 2 ** 4, k_update: int = 8, angle: float = None):
+        """The thesis-results driver ("Ours", PostProcessing.ipynb:1069-1090): per iteration the feature decomposition,
+        then flat_step (alpha[0]) on flat points and feature_step (alphas[1], alphas[2]) on edge and corner points, all
+        computed from the iteration's input positions (Jacobi across classes: temp_pos = pos.clone()), with the per-step
+        clamp at d * step_clamp_factor (effectively off) and a GLOBAL clamp: a point takes its new position only while
+        it stays within d of its position when this call started (mask = ||temp_pos - original_pos|| < d), else it
+        keeps its current one.  d defaults to 2 x the mean kNN(6) edge length, as in the notebook."""
+        if d is None:
+            d = 2 * float(self.meanEdgeLength())
+        phases = ((0, _nat.STEP_FLAT, alphas[0]), (1, _nat.STEP_FEATURE, alphas[1]), (2, _nat.STEP_FEATURE, alphas[2]))
+        g = self.graph
+        GeneralUtils.validateAttributes(g, ["pos", "n"])
+        fused = self._fused_for(max(k, k_update))
+        fused.load(g.pos, g.n)
+        params = _nat.make_params(k=k, k_update=k_update, rho=angle, d=float(d) * step_clamp_factor, phases=phases,
+                                  jacobi=True, clamp_global=float(d))
+        fused.iterate(params, iterations)
+        dev = _nat.device()
+        pos_out = torch.empty((g.num_nodes, 3), dtype=torch.float32, device=dev)
+        n_out = torch.empty((g.num_nodes, 3), dtype=torch.float32, device=dev)
+        fused.store(pos_out, n_out)
+        with torch.no_grad():
+            g.pos.copy_(pos_out.to(g.pos.dtype))
+        g.n = n_out.to(device=g.pos.device, dtype=g.pos.dtype)
+
     def denoiseUntilMinimumError(self, gt_pos: torch.Tensor, strategy: dict, k: int = 7,
                                  alpha: list = [0.02, 0.02, 0.1], d: float = 200,
                                  error_funcs: list[Callable] = [TorchUtils.PaperDistance], N: int = 2 ** 4):

@@ -84,6 +84,16 @@ class TorchUtils:
         return torch.cat([c0, c1], dim=0).to(pos0.device)
 
     @classmethod
+    def SingleChamferDistance(cls, pos0: torch.Tensor, pos1: torch.Tensor) -> torch.Tensor:
+        """sCD: the first half of ChamferDistance, ||pos0[nn0(pos1)] - pos1||² for every point of pos1 (len |pos1|).
+        With the reference's call order error_func(gt, denoised) (Processor.py:154,165, PostProcessing.ipynb:1024) this
+        is the denoised -> ground-truth term.  The reference notebook calls TorchUtils.SingleChamferDistance, which its
+        Utils.py does not define; this is that half of Utils.py:253-265."""
+        assert pos0.dim() == 2 and pos1.dim() == 2 and pos0.size(1) == 3 and pos1.size(1) == 3
+        c0, _ = _nn(pos0, pos1)
+        return c0.to(pos0.device)
+
+    @classmethod
     def HausdorffDistance(cls, pos0: torch.Tensor, pos1: torch.Tensor) -> torch.Tensor:
         assert pos0.dim() == 2 and pos1.dim() == 2 and pos0.size(1) == 3 and pos1.size(1) == 3
         c0, _ = _nn(pos0, pos1)

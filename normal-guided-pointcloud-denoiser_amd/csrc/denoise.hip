@@ -101,11 +101,12 @@ struct RegNb32 {
 };
 
 __global__ void k_load(const float* __restrict__ pos, const float* __restrict__ n, const int32_t* __restrict__ perm,
-                       int64_t N, float4* __restrict__ pos_s, float4* __restrict__ n_s) {
+                       int64_t N, float4* __restrict__ pos_s, float4* __restrict__ n_s, float4* __restrict__ orig) {
     const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (r >= N) return;
     const int64_t i = perm[r];
     pos_s[r] = make_float4(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2], 0.f);
+    orig[r] = pos_s[r];
     n_s[r] = make_float4(n[3 * i], n[3 * i + 1], n[3 * i + 2], 0.f);
 }
 
@@ -545,7 +546,8 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
                                                 const float4* __restrict__ fn, const float4* __restrict__ edge,
                                                 const int32_t* __restrict__ idx, int64_t N, RowMap rm, int ku,
                                                 const uint8_t* __restrict__ cls, int c, const float* __restrict__ g,
-                                                float d, float alpha, int win) {
+                                                float d, float alpha, int win, int copy_others,
+                                                const float4* __restrict__ orig, float clampg) {
     // the flat phase moves most rows: its neighbour rows come from an LDS window of pin / fn around the block
     constexpr bool WIN = PCD_PHASE_WIN && (KIND == PCD_STEP_FLAT);
     __shared__ float4 s_pos[WIN ? WinSize<kWinHaloPhase>::rows : 1], s_fn[WIN ? WinSize<kWinHaloPhase>::rows : 1];
@@ -556,7 +558,10 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 p4 = pin[i];
-    if (cls[i] != c) { pout[i] = p4; return; }
+    if (cls[i] != c) {                  // Gauss-Seidel: every phase copies the others; Jacobi: only the first
+        if (copy_others) pout[i] = p4;
+        return;
+    }
     const Vec3 vi = v3(p4.x, p4.y, p4.z);
     const Rows4 P{pin}, F{fn};
     const ColNb nb{idx, N, i};
@@ -570,6 +575,11 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     else if (KIND == PCD_STEP_NEW) o = step_feature<true, KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
     else if (KIND == PCD_STEP_CORNER) o = step_corner<KU>(P, F, vi, ku, nb, d, alpha);
     else o = vi;
+    if (clampg > 0.f) {                 // global clamp against the loaded positions (PostProcessing.ipynb:1088-1089)
+        const float4 o4 = orig[i];
+        const bool keep = sqrtf(sq3(o - v3(o4.x, o4.y, o4.z))) < clampg;
+        o = keep ? o : vi;
+    }
     store4(pout, i, o);
 }
 
@@ -592,6 +602,7 @@ struct pcd_denoiser {
     int64_t n = 0;
     int kcap = 0;                 // columns of the stored kNN list
     float4 *pos[2] = {nullptr, nullptr}, *nrm = nullptr, *fn = nullptr, *edge = nullptr;
+    float4* orig = nullptr;       // positions at load(): the global clamp's reference (pcd_denoise_params)
     int cur = 0;                  // pos[cur] holds the current positions
     int32_t* idx = nullptr;
     uint8_t* cls = nullptr;
@@ -634,6 +645,8 @@ static int check_params(const pcd_denoiser* dn, const pcd_denoise_params* p) {
     PCD_CHECK_ARG(std::max(p->k, p->k_update) <= dn->kcap, "k / k_update exceed the k_max given at create");
     PCD_CHECK_ARG(std::max(p->k, p->k_update) <= dn->n, "k exceeds the number of points");
     PCD_CHECK_ARG(p->nphases >= 0 && p->nphases <= 3, "nphases must be 0..3");
+    PCD_CHECK_ARG(p->jacobi == 0 || p->jacobi == 1, "jacobi must be 0 or 1");
+    PCD_CHECK_ARG(!(p->clamp_global < 0.f), "clamp_global must be >= 0");
     for (int ph = 0; ph < p->nphases; ++ph) {
         PCD_CHECK_ARG(p->phase_class[ph] >= 0 && p->phase_class[ph] <= 2, "phase class must be 0, 1 or 2");
         PCD_CHECK_ARG(p->phase_kind[ph] >= PCD_STEP_FLAT && p->phase_kind[ph] <= PCD_STEP_DUMMY, "bad phase kind");
@@ -825,9 +838,10 @@ static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, co
     const float a = p->phase_alpha[ph];
     float4* pin = dn->pos[dn->cur];
     float4* pout = dn->pos[dn->cur ^ 1];
+    const int copy_others = (!p->jacobi || ph == 0) ? 1 : 0;
     if (rm.nq > 0) {
         const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
-#define PCD_PH2(KD, C) hipLaunchKernelGGL((k_phase<KD, C>), grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, dn->n, rm, p->k_update, dn->cls, c, gs, p->d, a, dn->windows)
+#define PCD_PH2(KD, C) hipLaunchKernelGGL((k_phase<KD, C>), grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, dn->n, rm, p->k_update, dn->cls, c, gs, p->d, a, dn->windows, copy_others, dn->orig, p->clamp_global)
 #define PCD_PH(KD)                                                                                                     \
     switch (knn_cap(p->k_update)) {                                                                                    \
         case 8: PCD_PH2(KD, 8); break;                                                                                 \
@@ -847,11 +861,12 @@ static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, co
 #undef PCD_PH2
         PCD_LAUNCH_CHECK();
     }
-    dn->cur ^= 1;
+    if (!p->jacobi) dn->cur ^= 1;    // Jacobi: every phase reads the same input; the swap happens at finish
     return PCD_OK;
 }
 
-static void stage_finish(pcd_denoiser* dn) {
+static void stage_finish(pcd_denoiser* dn, const pcd_denoise_params* p) {
+    if (p->jacobi && p->nphases > 0) dn->cur ^= 1;
     std::swap(dn->nrm, dn->fn);   // graph.n = f_n  (Processor.py:139)
     dn->iterated = true;
 }
@@ -882,6 +897,7 @@ int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out) {
               hipMalloc(&dn->nrm, N * sizeof(float4)) == hipSuccess &&
               hipMalloc(&dn->fn, N * sizeof(float4)) == hipSuccess &&
               hipMalloc(&dn->edge, N * sizeof(float4)) == hipSuccess &&
+              hipMalloc(&dn->orig, N * sizeof(float4)) == hipSuccess &&
               hipMalloc(&dn->idx, (int64_t)k_max * N * sizeof(int32_t)) == hipSuccess &&
               hipMalloc(&dn->cls, N) == hipSuccess &&
               hipMalloc(&dn->part, kNumPart * sizeof(RedC)) == hipSuccess &&
@@ -900,7 +916,7 @@ int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out) {
 int pcd_denoiser_destroy(pcd_denoiser* dn) {
     if (!dn) return PCD_OK;
     (void)hipFree(dn->pos[0]); (void)hipFree(dn->pos[1]); (void)hipFree(dn->nrm); (void)hipFree(dn->fn);
-    (void)hipFree(dn->edge); (void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part);
+    (void)hipFree(dn->edge); (void)hipFree(dn->orig); (void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part);
     (void)hipFree(dn->red); (void)hipFree(dn->gscal); (void)hipFree(dn->err);
     (void)hipFree(dn->anc); (void)hipFree(dn->alist); (void)hipFree(dn->redo); (void)hipFree(dn->spill);
     (void)hipFree(dn->rqs); (void)hipFree(dn->fail); (void)hipFree(dn->sel_tmp);
@@ -912,7 +928,7 @@ int pcd_denoiser_destroy(pcd_denoiser* dn) {
 int pcd_denoiser_load(pcd_denoiser* dn, const float* pos, const float* n, void* stream) {
     PCD_CHECK_ARG(dn && pos && n, "null argument");
     hipLaunchKernelGGL(k_load, dim3((unsigned)cdiv(dn->n, 256)), dim3(256), 0, as_stream(stream), pos, n,
-                       dn->g->perm, dn->n, dn->pos[0], dn->nrm);
+                       dn->g->perm, dn->n, dn->pos[0], dn->nrm, dn->orig);
     PCD_LAUNCH_CHECK();
     dn->cur = 0;
     dn->loaded = true;
@@ -984,7 +1000,7 @@ int pcd_denoiser_stage(pcd_denoiser* dn, const pcd_denoise_params* p, int stage,
         case PCD_STAGE_PHASE_CENTRE: return stage_centre(dn, phase, static_cast<const double*>(red), st);
         case PCD_STAGE_PHASE_MAXDIST: return stage_maxdist(dn, p, phase, static_cast<float*>(red), st);
         case PCD_STAGE_PHASE_APPLY: return stage_apply(dn, p, phase, static_cast<const float*>(red), st);
-        default: stage_finish(dn); return PCD_OK;
+        default: stage_finish(dn, p); return PCD_OK;
     }
 }
 
@@ -1114,7 +1130,7 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
         }
         if (ev)
             for (int ph = p->nphases; ph < 3; ++ph) PCD_HIP(hipEventRecord(ev[3 + ph], st));
-        stage_finish(dn);
+        stage_finish(dn, p);
         if (ev) PCD_HIP(hipEventRecord(ev[6], st));
         if (ev) PCD_HIP(hipEventRecord(ev[7], st));
     }

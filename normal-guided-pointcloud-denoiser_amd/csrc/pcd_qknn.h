@@ -113,9 +113,62 @@ PCD_DEV unsigned long long rfl64(unsigned long long v) {
     return (unsigned long long)rfl((uint32_t)v) | ((unsigned long long)rfl((uint32_t)(v >> 32)) << 32);
 }
 
+// Shrink a survivor set of more than 128 to at most 128 before ordering it (a 2-slot sort instead of 4): a few
+// bisection steps on d² find a bound with KA <= count(d² <= bound) <= 128; the keys under it contain the KA best
+// of the whole set (at least KA keys are under it), so the compaction never changes the result.
+template <int KA>
+PCD_DEV float rq_shrink(unsigned long long* buf, int& cnt, float capd2, int lane) {
+    if (cnt <= 128) return -1.f;
+    wave_sync();
+    float d[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int e = s * 64 + lane;
+        d[s] = e < cnt ? __uint_as_float((uint32_t)(buf[e] >> 32)) : 3.0e38f;
+    }
+    auto count_le = [&](float t) {
+        int c = 0;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) c += __popcll(__ballot(d[s] <= t));
+        return c;
+    };
+    float lo = 0.f, hi = capd2, bound = -1.f;
+#pragma unroll 1
+    for (int it = 0; it < 8; ++it) {
+        const float mid = 0.5f * (lo + hi);
+        const int c = count_le(mid);
+        if (c < KA) lo = mid;
+        else if (c > 128) hi = mid;
+        else { bound = mid; break; }
+    }
+    if (bound < 0.f) return -1.f;                     // no such bound found quickly: order the full set
+    unsigned long long keep[4];
+    int base = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) keep[s] = (s * 64 + lane) < cnt ? buf[s * 64 + lane] : 0ull;
+    wave_sync();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const bool in = d[s] <= bound;
+        const unsigned long long m = __ballot(in);
+        if (in) buf[base + __popcll(m & ((1ull << lane) - 1ull))] = keep[s];
+        base += __popcll(m);
+    }
+    cnt = base;
+    return bound;
+}
+
 // Cut the survivors to the K best (quantised order): false when the cut is ambiguous (the query must spill).
 template <int K>
 PCD_DEV bool rq_cut(unsigned long long* buf, int& cnt, unsigned long long& cap, int lane) {
+    {
+        const float bound = rq_shrink<K>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lane);
+        if (bound >= 0.f) {                           // >= K keys have d² <= bound: a valid, tighter cap
+            const unsigned long long c2 = ((unsigned long long)__float_as_uint(bound) << 32) | 0xFFFFFFFFull;
+            if (c2 < cap) cap = c2;
+            return true;
+        }
+    }
     uint32_t after;
     const uint32_t k = wave_order32(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lane, after);
     const uint32_t kK = K < 64 ? (uint32_t)__shfl((int)k, K < 64 ? K : 0) : after;
@@ -290,14 +343,15 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
         const float4 p4 = pos[i];
         const Vec3 q = v3(p4.x, p4.y, p4.z);
         unsigned long long cap;
+        float r_dense = 0.f;
         if (DENSE) {
             const int cx = min(max(cell_coord(q.x, g.ox, g.inv_h), 0), g.dx - 1);
             const int cy = min(max(cell_coord(q.y, g.oy, g.inv_h), 0), g.dy - 1);
             const int cz = min(max(cell_coord(q.z, g.oz, g.inv_h), 0), g.dz - 1);
             uint32_t s = 0, e = 0;
             const int n = cell_range(g, cx, cy, cz, s, e) ? (int)(e - s) : 1;
-            const float r = r_scale * g.h * cbrtf(16.f / (float)n);
-            cap = ((unsigned long long)__float_as_uint(r * r) << 32) | 0xFFFFFFFFull;
+            r_dense = r_scale * g.h * cbrtf(16.f / (float)n);
+            cap = ((unsigned long long)__float_as_uint(r_dense * r_dense) << 32) | 0xFFFFFFFFull;
         } else {
             const float4 a = anc[i];
             if (!(a.w >= 0.f)) {                      // no anchor: the wave search grows its own box
@@ -306,16 +360,31 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
             }
             cap = anchor_cap(q, a);
         }
-        const float rr = sqrtf(__uint_as_float((unsigned)(cap >> 32))) * 1.0001f + 1e-30f;
-        int lo[3], hi[3];
-        cell_box(g, q, rr, lo, hi);
         int cnt = 0;
-        const int64_t nbox = (int64_t)(hi[0] - lo[0] + 1) * (hi[1] - lo[1] + 1) * (hi[2] - lo[2] + 1);
-        const bool big = nbox > kRqMaxCells;
-        bool ok = !big && rq_scan_box<KA>(g, q, lo, hi, cap, buf, cnt, &s_cells[wv], lane) && cnt >= KA;
+        bool big = false, ok = false;
+        // dense: a radius guess holding fewer than KA points is widened (x 1.6, twice) before the query spills
+#pragma unroll 1
+        for (int attempt = 0; attempt < (DENSE ? 3 : 1); ++attempt) {
+            if (attempt > 0) {
+                r_dense *= 1.6f;
+                cap = ((unsigned long long)__float_as_uint(r_dense * r_dense) << 32) | 0xFFFFFFFFull;
+            }
+            const float rr = sqrtf(__uint_as_float((unsigned)(cap >> 32))) * 1.0001f + 1e-30f;
+            int lo[3], hi[3];
+            cell_box(g, q, rr, lo, hi);
+            cnt = 0;
+            const int64_t nbox = (int64_t)(hi[0] - lo[0] + 1) * (hi[1] - lo[1] + 1) * (hi[2] - lo[2] + 1);
+            big = nbox > kRqMaxCells;
+            if (big) break;
+            const bool clean = rq_scan_box<KA>(g, q, lo, hi, cap, buf, cnt, &s_cells[wv], lane);
+            ok = clean && cnt >= KA;
+            if (ok || !clean) break;
+            wave_sync();
+        }
         uint32_t k = 0xFFFFFFFFu;
         if (ok) {
             uint32_t after;
+            (void)rq_shrink<KA>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lane);
             k = wave_order32(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lane, after);
             // exact order of the stored list (first kstore + its successor) and of the anchor set boundary
             ok = order_exact(k, after, kstore, lane);

@@ -36,7 +36,7 @@ class DenoiseParams(ctypes.Structure):
     """Mirror of ``pcd_denoise_params`` (include/pcd.h)."""
     _fields_ = [("k", c_int), ("k_update", c_int), ("rho", c_float), ("tau", c_float), ("damp", c_float),
                 ("class_scale", c_float), ("d", c_float), ("nphases", c_int), ("phase_class", c_int * 3),
-                ("phase_kind", c_int * 3), ("phase_alpha", c_float * 3)]
+                ("phase_kind", c_int * 3), ("phase_alpha", c_float * 3), ("jacobi", c_int), ("clamp_global", c_float)]
 
 
 # name -> (restype, argtypes); the exact export list of include/pcd.h
@@ -355,7 +355,8 @@ class FusedDenoiser:
 
 
 def make_params(k=16, k_update=8, rho=None, tau=0.3, damp=3.0, class_scale=0.2, d=1.0,
-                phases=((0, STEP_FLAT, 1.0), (1, STEP_EDGE, 0.2), (2, STEP_FEATURE, 1.0))) -> DenoiseParams:
+                phases=((0, STEP_FLAT, 1.0), (1, STEP_EDGE, 0.2), (2, STEP_FEATURE, 1.0)), jacobi=False,
+                clamp_global=0.0) -> DenoiseParams:
     import math
     p = DenoiseParams()
     p.k, p.k_update = int(k), int(k_update)
@@ -364,6 +365,8 @@ def make_params(k=16, k_update=8, rho=None, tau=0.3, damp=3.0, class_scale=0.2, 
     p.nphases = len(phases)
     for t, (c, kind, a) in enumerate(phases):
         p.phase_class[t], p.phase_kind[t], p.phase_alpha[t] = int(c), int(kind), float(a)
+    p.jacobi = int(bool(jacobi))
+    p.clamp_global = float(clamp_global)
     return p
 
 

@@ -256,7 +256,8 @@ class SlabDenoiser:
                 e.stage(params, nat.STAGE_PHASE_APPLY, ph, red1)
             else:
                 e.stage(params, nat.STAGE_PHASE_APPLY, ph, None)
-            self._exchange(nat.FIELD_POS)
+            if not params.jacobi:          # Gauss-Seidel: the next phase reads these positions
+                self._exchange(nat.FIELD_POS)
 
     def iterate(self, params, iterations: int = 1):
         e = self.e
@@ -266,6 +267,8 @@ class SlabDenoiser:
             e.stage(params, nat.STAGE_NVT2)
             self._phases(params)
             e.stage(params, nat.STAGE_FINISH)
+            if params.jacobi:              # Jacobi across classes: one position refresh per iteration
+                self._exchange(nat.FIELD_POS)
 
     def iterate_timed(self, params) -> dict:
         """One iteration with CUDA/HIP events on the launch stream around each stage group (ms)."""
@@ -281,6 +284,8 @@ class SlabDenoiser:
         self._phases(params)
         ev[4].record()
         e.stage(params, nat.STAGE_FINISH)
+        if params.jacobi:
+            self._exchange(nat.FIELD_POS)
         ev[5].record()
         ev[5].synchronize()
         names = ["knn_nvt1", "fn_exchange", "nvt2", "phases_with_exchange", "finish"]

@@ -17,6 +17,12 @@ Every fixture records which reference entry point produced it:
   lattice.npz       FeatureFix.ipynb lattice-cube known-answer test (n=9, 17; exact and 1e-4 jittered)
   mesh_update.npz   Mesh.updateVertices (PatchGeneration/Modules/Mesh.py:377-418) on the fandisk mesh
   metrics.npz       TorchUtils.ChamferDistance / PaperDistance / averageEdgeLength (Utils.py:253-299)
+  until_min.npz     Processor.denoiseUntilMinimumError (Processor.py:141-185) on fandisk: strategy {0: flat_step,
+                    1: edge_step, 2: feature_step}, k=8, alpha=[1, 0.2, 1], d=2l, error PaperDistance; the returned
+                    pos / errors / iteration count and the error trajectory
+  thesis.npz        the thesis driver "Ours" (PostProcessing.ipynb:1069-1090) on fandisk: 2 iterations, Jacobi
+                    across classes, flat_step + feature_step at d*20000, global clamp ||temp_pos - original_pos|| < d
+  io.npz            Object.Pointcloud.loadObj readback of models/fandisk.obj (Object.py:71-89)
 """
 from __future__ import annotations
 
@@ -346,8 +352,76 @@ def gen_cpsd(out_dir):
           f"VU classes {np.bincount(res['vu_classes'], minlength=3)}, corners {len(corners)}")
 
 
+def gen_until_min(out_dir):
+    f = np.load(os.path.join(out_dir, "fandisk_k32.npz"))
+    pos0 = torch.from_numpy(f["pos0"])
+    n0 = torch.from_numpy(f["n0"])
+    gt = torch.from_numpy(f["gt"])
+    pc = Pointcloud(pos0.clone(), n0.clone())
+    proc = Processor(pc)
+    l = TorchUtils.averageEdgeLength(proc.graph.pos, proc.selector.getKNNSelection(6).getEdgeIndex())
+    d = float(2 * l)
+    traj = []
+
+    def err(gt_pos, pos):
+        e = TorchUtils.PaperDistance(gt_pos, pos)
+        traj.append(float(e.mean()))
+        return e
+
+    den = proc.denoiser
+    strategy = {0: den.flat_step, 1: den.edge_step, 2: den.feature_step}
+    pos, errors, iters = proc.denoiseUntilMinimumError(gt, strategy, k=8, alpha=[1, 0.2, 1], d=d, error_funcs=[err])
+    np.savez_compressed(os.path.join(out_dir, "until_min.npz"), pos0=f["pos0"], n0=f["n0"], gt=f["gt"],
+                        d=np.float64(d), pos=np32(pos), errors=np32(errors[0]), iterations=np.int64(iters),
+                        trajectory=np.asarray(traj), pc_v=np32(pc.v), graph_pos=np32(proc.graph.pos))
+    print(f"until_min: d={d:.5f} iterations={iters} error trajectory {['%.4g' % x for x in traj]}")
+
+
+def gen_thesis(out_dir):
+    """PostProcessing.ipynb:1069-1090 (j == 3, "Ours") verbatim on fandisk."""
+    f = np.load(os.path.join(out_dir, "fandisk_k32.npz"))
+    col_value = Processor(Pointcloud(torch.from_numpy(f["pos0"]).clone(), torch.from_numpy(f["n0"]).clone()))
+    l = TorchUtils.averageEdgeLength(col_value.graph.pos, col_value.selector.getKNNSelection(6).getEdgeIndex())
+    d = 2 * l
+    original_pos = col_value.graph.pos.clone()
+    res = {"pos0": f["pos0"], "n0": f["n0"], "d": np.float64(d)}
+    alphas = [1, 0.2, 1]
+    for it in range(2):
+        decomposition, f_n = col_value.getMyFeatureDecomposition()
+        classes = decomposition.getClasses()
+        selection = col_value.selector.getKNNSelection(8)
+        temp_pos = col_value.graph.pos.clone()
+        for key in range(3):
+            indices = (classes == key).nonzero().flatten()
+            if indices.size(0) == 0:
+                continue
+            elif key == 0:
+                new_pos = col_value.denoiser.flat_step(selection.filter(indices), f_n, d * 20000, alphas[key])
+            else:
+                new_pos = col_value.denoiser.feature_step(selection.filter(indices), f_n, d * 20000, alphas[key])
+            temp_pos[indices] = new_pos
+        mask = (temp_pos - original_pos).norm(dim=1) < d
+        col_value.graph.pos[mask] = temp_pos[mask]
+        col_value.graph.n = f_n
+        res[f"pos_it{it + 1}"] = np32(col_value.graph.pos)
+        res[f"n_it{it + 1}"] = np32(col_value.graph.n)
+        res[f"classes_it{it + 1}"] = classes.numpy()
+        res[f"mask_it{it + 1}"] = mask.numpy()
+    np.savez_compressed(os.path.join(out_dir, "thesis.npz"), **res)
+    print(f"thesis: d={float(d):.5f} masked-out after 2 iterations: {int((~res['mask_it2']).sum())}")
+
+
+def gen_io(out_dir):
+    """Pointcloud.loadObj (Object.py:71-89) on models/fandisk.obj: the vertex array the reference reads (igl is
+    absent here: refshim's OBJ reader stands in for igl.read_triangle_mesh, so this pins the readback of the file's
+    `v` lines and the face count)."""
+    v, faces = refshim.read_obj(f"{REF}/models/fandisk.obj")
+    np.savez_compressed(os.path.join(out_dir, "io.npz"), v=np.asarray(v, np.float32), f=np.asarray(faces, np.int32))
+    print(f"io: fandisk.obj V={len(v)} F={len(faces)}")
+
+
 GENS = {"fandisk": gen_fandisk, "steps": gen_steps, "lattice": gen_lattice, "mesh": gen_mesh,
-        "metrics": gen_metrics, "cpsd": gen_cpsd}
+        "metrics": gen_metrics, "cpsd": gen_cpsd, "until_min": gen_until_min, "thesis": gen_thesis, "io": gen_io}
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
