@@ -16,8 +16,12 @@ along its longest axis; each rank denoises its slab and exchanges halo state wit
 runs N independent P-point clouds.  The timed region is bracketed by barrier + synchronize and the max over
 ranks is reported.
 
-The JSON line carries `roofline` for the dominant kernel (fused kNN + NVT1, HIP events on its own stream) and
-`cpu_baseline` (the oracle restatement on host cores over a bounded sample; rank 0, N = 1 only).
+The JSON line carries `roofline` for the dominant stage (K1 = kNN + NVT1, HIP events on its launch stream),
+`kernel_ms` per stage (HIP events), `ten_iteration_ms` (a fresh cloud through configs[3]'s 10 iterations, the dense
+first anchoring included), `measured_traffic` (the rocprofv3 PMC bytes of profiles/traffic.json per iteration against
+8 TB/s), `cpu_baseline` (the oracle restatement on host cores over a bounded sample) and `parity` (the same sample
+through one GPU iteration: Chamfer distance to the clean surface vs the oracle's, class agreement); the last two on
+rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
@@ -43,6 +47,23 @@ from Pointcloud.Modules.Processor import Processor  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
+# Per-stage bound, as the rocprofv3 counters of profiles/ show it: VALU = VALU-issue-bound (>= 1/2 of
+# the SIMD's VALU issue busy), latency = memory-latency-bound (SQ wait > 0.6 of wave cycles at full occupancy).
+STAGE_BOUND = {"anchor_test": "valu", "requery": "latency+valu", "spill_search": "latency", "nvt1": "valu",
+               "nvt2": "valu", "flat_phase": "latency", "edge_phase": "latency", "corner_phase": "latency",
+               "finish": "-"}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def knn_cap(k):
     """Register list size the fused kernel is instantiated with (pcd_denoiser_iterate)."""
     return 8 if k <= 8 else 16 if k <= 16 else 32 if k <= 32 else 64
@@ -52,7 +73,8 @@ def k1_kernels(k, ku, seeding, anchoring):
     """Kernels of the K1 stage (kNN + NVT1) as pcd_denoiser_iterate launches them in a timed (seeded) step."""
     c = knn_cap(max(k, ku))
     if seeding and anchoring and c <= 32:
-        return [f"k_knn_anchor<{c}, {2 * c}>", f"k_knn_redo_wave<{2 * c}, false>", f"k_nvt1<{c}>"]
+        return [f"k_knn_anchor<{c}, {2 * c}>", f"k_knn_requery<{2 * c}, false>", f"k_knn_redo_wave<{2 * c}, false>",
+                f"k_nvt1<{c}>"]
     return [f"k_knn_nvt1<{c}, {'true' if seeding else 'false'}>"]
 
 
@@ -67,36 +89,76 @@ def b_alg_knn_nvt1(k):
     return 12 + 12 * k + 4 * k + 24 * k + 12 + 12
 
 
-def make_cloud(n, seed, dev, sigma_frac=0.005):
+def make_cloud(n, seed, dev, sigma_frac=0.005, clean=False):
     m = np.load(os.path.join(ROOT, "data", "stanford_bunny_mesh.npz"))
     v = torch.from_numpy(m["v"]).to(dev)
     f = torch.from_numpy(m["f"].astype(np.int64)).to(dev)
     g = torch.Generator(device=dev).manual_seed(seed)
-    pos, nrm = sample_surface(v, f, n, generator=g)
+    surf, nrm = sample_surface(v, f, n, generator=g)
     diag = float((v.max(0).values - v.min(0).values).norm())
-    pos = pos + sigma_frac * diag * torch.randn(pos.shape, generator=g, device=dev)
+    pos = surf + sigma_frac * diag * torch.randn(surf.shape, generator=g, device=dev)
+    if clean:
+        return pos.contiguous(), nrm.contiguous(), diag, surf.contiguous()
     return pos.contiguous(), nrm.contiguous(), diag
 
 
-def cpu_baseline(k, ku, sample_points, seed=99):
-    """The oracle (numpy/scipy restatement of the reference, cKDTree workers=1) on a bounded sample."""
+def cpu_baseline(k, ku, sample_points, dev, seed=99):
+    """The oracle (numpy/scipy restatement of the reference, cKDTree workers=1) for one iteration on a bounded sample,
+    and the same sample through one fused GPU iteration: (cpu_baseline, parity) blocks of the JSON line."""
     from oracle import pcd_oracle as O
     # the host share this process may use: affinity mask, capped by OMP_NUM_THREADS (16 on the GPU box)
     threads = len(os.sched_getaffinity(0))
     if os.environ.get("OMP_NUM_THREADS", "").isdigit():
         threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
     torch.set_num_threads(threads)
-    pos, nrm, _ = make_cloud(sample_points, seed, torch.device("cpu"))
+    pos, nrm, _, surf = make_cloud(sample_points, seed, torch.device("cpu"), clean=True)
     pos, nrm = pos.numpy(), nrm.numpy()
     knn = O.FrozenKNN(pos)
     d = 2 * O.mean_edge_length(pos, knn)
     t0 = time.perf_counter()
-    O.denoise_iteration(pos, nrm, knn, d, k, ku)
+    rpos, _, rcls = O.denoise_iteration(pos, nrm, knn, d, k, ku)
     dt = time.perf_counter() - t0
-    return {"value": round(sample_points / dt / 1e6, 5), "unit": "Mpoints/s", "cores": threads, "kind": "port",
+    base = {"value": round(sample_points / dt / 1e6, 5), "unit": "Mpoints/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"1 iteration of the oracle restatement on {sample_points:,} bunny-sampled points "
                       f"(k={k}, k_u={ku}), scipy cKDTree workers=1, torch intra-op threads={threads}, "
                       f"{dt:.2f} s"}
+    # parity on the same sample: one fused GPU iteration, Chamfer distance to the noiseless surface samples
+    from Pointcloud.Modules.Utils import TorchUtils
+    proc = Processor(Pointcloud(torch.from_numpy(pos).to(dev), torch.from_numpy(nrm).to(dev)), k_hint=k)
+    fused = proc._fused_for(max(k, ku))
+    fused.load(proc.graph.pos, proc.graph.n)
+    fused.iterate(nat.make_params(k=k, k_update=ku, d=d), 1)
+    gp = torch.empty((sample_points, 3), device=dev)
+    gc = torch.empty(sample_points, dtype=torch.int64, device=dev)
+    fused.store(gp, None, gc)
+    gt = surf.to(dev)
+    cd_gpu = float(TorchUtils.ChamferDistance(gt, gp).mean())
+    cd_ref = float(TorchUtils.ChamferDistance(gt, torch.from_numpy(rpos).to(dev)).mean())
+    cd_in = float(TorchUtils.ChamferDistance(gt, torch.from_numpy(pos).to(dev)).mean())
+    parity = {"sample": f"the cpu_baseline sample ({sample_points:,} points), 1 iteration, Chamfer distance to the "
+                        f"noiseless surface samples", "cd_noisy": cd_in, "cd_oracle": cd_ref, "cd_gpu": cd_gpu,
+              "cd_delta_rel": abs(cd_gpu - cd_ref) / cd_ref,
+              "class_agreement": float((gc.cpu().numpy() == rcls).mean())}
+    return base, parity
+
+
+def measured_traffic(points, k, ms_per_step):
+    """HBM bytes per iteration from profiles/traffic.json (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch, the
+    gfx950 correction of MI355X_MICROARCH.md), summed over the iteration's kernels, against 8 TB/s."""
+    tfile = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(tfile):
+        return None
+    try:
+        tj = json.load(open(tfile))
+    except (OSError, ValueError):
+        return None
+    if tj.get("points") != points or tj.get("k") != k or "per_iteration_bytes" not in tj:
+        return None
+    b = float(tj["per_iteration_bytes"])
+    return {"bytes_per_iteration": b, "achieved": round(b / (ms_per_step / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(b / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "source": tj.get("source", "profiles/traffic.json")}
 
 
 def main():
@@ -117,6 +179,11 @@ def main():
                     help="slab mode: extra per-stage timed iterations after the timed region (torch events)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: independent clouds per rank instead of spatial slabs of one global cloud")
+    ap.add_argument("--strong", action="store_true",
+                    help="N > 1 slabs: one global cloud of --points in total (strong scaling, BASELINE configs[4] "
+                         "asks for 80M), instead of --points per GPU")
+    ap.add_argument("--no-ten", dest="ten", action="store_false",
+                    help="skip the ten_iteration_ms measurement (fresh cloud, 10 iterations incl. the first)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -139,7 +206,8 @@ def main():
     if mode == "slab":
         # one global cloud of world x P points (identical on every rank), cut into spatial slabs with a halo
         from pcd_slab import SlabDenoiser, TorchTransport
-        pos, nrm, diag = make_cloud(args.points * world, 3, dev)
+        total = args.points if args.strong else args.points * world
+        pos, nrm, diag = make_cloud(total, 3, dev)
         dist.broadcast(pos, 0)       # one cloud: rank 0's (device sampling is not bit-reproducible across ranks)
         dist.broadcast(nrm, 0)
         dt = torch.tensor([2 * float(Processor(Pointcloud(pos), k_hint=args.k).meanEdgeLength())], device=dev)
@@ -191,7 +259,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     ms_per_step = elapsed / args.steps * 1e3
-    total_points = args.points * world
+    total_points = args.points if (mode == "slab" and args.strong) else args.points * world
     value = total_points / (ms_per_step / 1e3) / 1e6
 
     # per-kernel timing (HIP events on the launch stream), outside the timed region
@@ -205,10 +273,23 @@ def main():
     else:
         slots = fused.timing()      # averages over exactly the timed iterations
         fused.set_timing(False)
+        fused.check()               # device error word: invalid list entries would fail the bench here
         if slots:
-            knn_ms = float(slots[0])
-            names = ["knn_nvt1", "nvt2", "flat_phase", "edge_phase", "corner_phase"]
-            kernel_ms = {names[i]: round(float(slots[i]), 4) for i in range(min(len(slots), 5))}
+            names = nat.FusedDenoiser.TIMING_SLOTS
+            kernel_ms = {names[i]: round(float(slots[i]), 4) for i in range(min(len(slots), len(names)))}
+            knn_ms = float(sum(slots[:4]))
+            kernel_ms["knn_nvt1"] = round(knn_ms, 4)
+    ten_ms = None
+    if mode != "slab" and args.ten:
+        # configs[3] as written: a fresh cloud (no anchors yet) through 10 iterations, the dense first one included
+        fused.load(proc.graph.pos, proc.graph.n)
+        fused.reset_seed()
+        torch.cuda.synchronize()
+        t10 = time.perf_counter()
+        fused.iterate(params, 10)
+        torch.cuda.synchronize()
+        ten_ms = (time.perf_counter() - t10) * 1e3
+        fused.check()
 
     k1_points = sd.owned_global.numel() if mode == "slab" else args.points
     k1_bytes = b_alg_knn_nvt1(args.k) * k1_points
@@ -220,8 +301,8 @@ def main():
         try:
             tj = json.load(open(tfile))
             if tj.get("points") == args.points and tj.get("k") == args.k:
-                per = [tj["kernels"][nm][0]["hbm_bytes_per_launch"] for nm in k1_names]
-                traffic = float(sum(per))
+                per = [tj["kernels"][nm][0]["hbm_bytes_per_launch"] for nm in k1_names if nm in tj["kernels"]]
+                traffic = float(sum(per)) if per else None
         except Exception:
             traffic = None
     iter_alg = b_alg_iteration(args.k, args.k_update) * args.points
@@ -234,7 +315,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if (mode == "slab" and args.strong) else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: bunny-sampled surface + Gaussian noise (sigma=0.005*bbox), analytic normals, "
@@ -243,24 +324,27 @@ def main():
                                 % (total_points // 1_000_000) if mode == "slab" else
                                 "configs[3] headline substitute: 10M-pt bunny-sampled cloud (xyzrgb_dragon.obj is "
                                 "a missing blob)") + ", k=32, k_u=8, 1 iteration per step",
-                   "points_per_gpu": args.points, "k": args.k, "k_update": args.k_update,
+                   "points_per_gpu": total_points // world, "k": args.k, "k_update": args.k_update,
                    "global_points": total_points,
                    "parallelism": {"single": "single", "replicas": f"replicas x{world}",
                                    "slab": f"spatial slabs x{world}"}[mode]},
         "iterations_per_sec": round(1e3 / ms_per_step, 2),
         "first_iteration_ms": round(first_ms, 3) if first_ms is not None else None,
+        "ten_iteration_ms": round(ten_ms, 3) if ten_ms is not None else None,
         "kernel_ms": kernel_ms,
+        "stage_bound": STAGE_BOUND if mode != "slab" else None,
         "iteration_roofline": {"bound": "hbm", "alg_bytes_per_point": b_alg_iteration(args.k, args.k_update),
                                "achieved": round(iter_alg / (ms_per_step / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
                                "unit": "GB/s",
                                "frac": round(iter_alg / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
-        "roofline": {"kernel": "K1 stage (kNN + NVT1): " + " + ".join(k1_names), "bound": "hbm",
+        "measured_traffic": measured_traffic(args.points, args.k, ms_per_step) if mode != "slab" else None,
+        "roofline": {"kernel": "K1 stage (kNN + NVT1): " + " + ".join(k1_names), "bound": "valu+latency",
                      "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                      "traffic": traffic, "alg_bytes_per_launch": k1_bytes, "avg_launch_ms": round(knn_ms, 4)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.k, args.k_update, args.cpu_sample)
+        out["cpu_baseline"], out["parity"] = cpu_baseline(args.k, args.k_update, args.cpu_sample, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

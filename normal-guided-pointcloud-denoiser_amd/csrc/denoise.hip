@@ -636,7 +636,9 @@ struct pcd_denoiser {
 };
 
 static const int kNumPart = 1024;
-static const int kTimingSets = 256, kTimingEvents = 8;
+// Timing events per iteration: start, after the anchor test (+ redo-list select), after the re-anchoring search,
+// after the exact-key spill search, after NVT1 (= end of K1), after NVT2, after each of 3 phases, after finish, end.
+static const int kTimingSets = 256, kTimingEvents = 11;
 
 static int check_params(const pcd_denoiser* dn, const pcd_denoise_params* p) {
     PCD_CHECK_ARG(dn && p, "null argument");
@@ -692,7 +694,8 @@ static int select_rows(pcd_denoiser* dn, const RowMap& rm, int32_t* list, unsign
 #ifndef PCD_RQ_GRID
 #define PCD_RQ_GRID 4096
 #endif
-static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int K, hipStream_t st) {
+static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int K, hipStream_t st,
+                             hipEvent_t* ev) {
     const int64_t N = dn->n;
     const RowMap rm = dn->rowmap();
     const int kstore = std::max(p->k, p->k_update);
@@ -722,17 +725,21 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
 #define PCD_K1A(C)                                                                                                     \
     case C:                                                                                                            \
         if (dense) {                                                                                                   \
+            if (ev) PCD_HIP(hipEventRecord(ev[1], st));                                                                \
             hipLaunchKernelGGL((k_knn_requery<2 * C, true>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, PCD_RQ_RDENSE,   \
                                dn->anc, dn->alist, dn->idx, dn->redo, redo_cnt, dn->spill, spill_cnt);                 \
         } else {                                                                                                       \
             hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd_anc, dim3(kAnchorBS), 0, st, gv, P, N, rm, kstore,        \
                                dn->anc, dn->alist, dn->idx, dn->fail);                                                 \
             if ((rc = select_rows(dn, rm, dn->redo, redo_cnt, st)) != PCD_OK) return rc;                               \
+            if (ev) PCD_HIP(hipEventRecord(ev[1], st));                                                                \
             hipLaunchKernelGGL((k_knn_requery<2 * C, false>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, 0.f, dn->anc,  \
                                dn->alist, dn->idx, dn->redo, redo_cnt, dn->spill, spill_cnt);                         \
         }                                                                                                              \
+        if (ev) PCD_HIP(hipEventRecord(ev[2], st));                                                                    \
         hipLaunchKernelGGL((k_knn_redo_wave<2 * C, false>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,       \
                            dn->alist, dn->idx, dn->spill, spill_cnt, dn->err);                                         \
+        if (ev) PCD_HIP(hipEventRecord(ev[3], st));                                                                    \
         hipLaunchKernelGGL((k_nvt1<C>), grd, blk, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore, p->rho, p->tau, \
                            p->damp, dn->cov, dn->fn, dn->err, dn->windows);                                          \
         break;
@@ -747,14 +754,15 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     return PCD_OK;
 }
 
-static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t st) {
+static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t st, hipEvent_t* ev = nullptr) {
     const int64_t N = dn->n;
     const RowMap rm = dn->rowmap();
-    if (rm.nq == 0) return PCD_OK;
     const int kstore = std::max(p->k, p->k_update);
     const int K = list_cap(p);
-    if (dn->seeding && dn->anchoring && K <= 32 && N >= 2 * K && knn_cap(dn->kcap) <= 32)
-        return stage_k1_anchored(dn, p, K, st);
+    if (rm.nq > 0 && dn->seeding && dn->anchoring && K <= 32 && N >= 2 * K && knn_cap(dn->kcap) <= 32)
+        return stage_k1_anchored(dn, p, K, st, ev);
+    if (ev) for (int e = 1; e <= 3; ++e) PCD_HIP(hipEventRecord(ev[e], st));   // no anchored sub-stages
+    if (rm.nq == 0) return PCD_OK;
     const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
     const GridView gv = dn->g->view;
     float4* P = dn->pos[dn->cur];
@@ -1114,10 +1122,10 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
         hipEvent_t* ev = nullptr;     // this iteration's event set (timing on, and a set left)
         if (dn->timing && dn->ev_used < kTimingSets) ev = &dn->ev[(size_t)dn->ev_used++ * kTimingEvents];
         if (ev) PCD_HIP(hipEventRecord(ev[0], st));
-        if ((rc = stage_k1(dn, p, st)) != PCD_OK) return rc;
-        if (ev) PCD_HIP(hipEventRecord(ev[1], st));
+        if ((rc = stage_k1(dn, p, st, ev)) != PCD_OK) return rc;
+        if (ev) PCD_HIP(hipEventRecord(ev[4], st));
         if ((rc = stage_k2(dn, p, st)) != PCD_OK) return rc;
-        if (ev) PCD_HIP(hipEventRecord(ev[2], st));
+        if (ev) PCD_HIP(hipEventRecord(ev[5], st));
         for (int ph = 0; ph < p->nphases; ++ph) {
             if (phase_is_global(p, ph)) {
                 double* red4 = dn->red + 4 * ph;
@@ -1126,13 +1134,13 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
                 if ((rc = stage_maxdist(dn, p, ph, nullptr, st)) != PCD_OK) return rc;
             }
             if ((rc = stage_apply(dn, p, ph, nullptr, st)) != PCD_OK) return rc;
-            if (ev) PCD_HIP(hipEventRecord(ev[3 + ph], st));
+            if (ev) PCD_HIP(hipEventRecord(ev[6 + ph], st));
         }
         if (ev)
-            for (int ph = p->nphases; ph < 3; ++ph) PCD_HIP(hipEventRecord(ev[3 + ph], st));
+            for (int ph = p->nphases; ph < 3; ++ph) PCD_HIP(hipEventRecord(ev[6 + ph], st));
         stage_finish(dn, p);
-        if (ev) PCD_HIP(hipEventRecord(ev[6], st));
-        if (ev) PCD_HIP(hipEventRecord(ev[7], st));
+        if (ev) PCD_HIP(hipEventRecord(ev[9], st));
+        if (ev) PCD_HIP(hipEventRecord(ev[10], st));
     }
     return PCD_OK;
 }

@@ -347,10 +347,14 @@ class FusedDenoiser:
         check(lib().pcd_denoiser_unpack(self.handle, int(field), ptr(rows), rows.numel(), ptr(data),
                                         c_void_p(stream_ptr())), "pcd_denoiser_unpack")
 
+    TIMING_SLOTS = ("anchor_test", "requery", "spill_search", "nvt1", "nvt2", "flat_phase", "edge_phase",
+                    "corner_phase", "finish")
+
     def timing(self):
-        buf = (c_float * 8)()
+        """Per-stage ms averaged over the iterations timed since set_timing / the last call (TIMING_SLOTS order)."""
+        buf = (c_float * 16)()
         nw = c_int(0)
-        check(lib().pcd_denoiser_get_timing(self.handle, buf, 8, ctypes.byref(nw)), "pcd_denoiser_get_timing")
+        check(lib().pcd_denoiser_get_timing(self.handle, buf, 16, ctypes.byref(nw)), "pcd_denoiser_get_timing")
         return [buf[i] for i in range(nw.value)]
 
 

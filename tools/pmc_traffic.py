@@ -48,9 +48,24 @@ def main():
         if fk is not None and wk is not None:
             entry["hbm_bytes_per_launch"] = (2.0 * fk + wk) * 1024.0
         kernels.setdefault(short(name), []).append(dict(entry, symbol=name))
+    # bytes of one seeded iteration: every per-iteration kernel's average bytes x its launches, over the number of
+    # iterations (= NVT2 launches); one-time kernels (grid build, load/store, the dense first re-anchoring) excluded
+    one_time = ("k_bbox", "k_sample", "k_keys", "k_gather_sorted", "k_count_starts", "k_brick_flags", "k_insert",
+                "k_load", "k_store", "k_edge_len", "k_knn<", "k_nn1", "k_radius", "true>")
+    n_iter = sum(e["launches_fetch"] for e in kernels.get("k_nvt2<32>", [])) or None
+    per_iter = None
+    if n_iter:
+        per_iter = 0.0
+        for kname, v in kernels.items():
+            if any(t in kname for t in one_time):
+                continue
+            for e in v:
+                if e.get("hbm_bytes_per_launch") is not None:
+                    per_iter += e["hbm_bytes_per_launch"] * e["launches_fetch"] / n_iter
     res = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, csv; "
                      "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch (gfx950 FETCH_SIZE counts half)",
-           "points": points, "k": k, "kernels": kernels}
+           "points": points, "k": k, "iterations": n_iter, "per_iteration_bytes": per_iter,
+           "source": os.path.relpath(fetch_csv), "kernels": kernels}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     for kname, v in kernels.items():

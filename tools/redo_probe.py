@@ -41,7 +41,7 @@ def main():
             ts = fused.tile_stats()
             extra += (f"  | spilled to the exact wave search {ts['spilled']} (big box {ts['spilled_big_box']}, "
                       f"ambiguous {ts['spilled_ambiguous']})")
-        print(f"it {it:3d}: redo {r:9d} ({r / n * 100:5.2f} %)  K1 {t[0]:7.3f} ms  iteration {sum(t):7.3f} ms{extra}",
+        print(f"it {it:3d}: redo {r:9d} ({r / n * 100:5.2f} %)  K1 {sum(t[:4]):7.3f} ms (requery {t[1]:6.3f})  iteration {sum(t):7.3f} ms{extra}",
               flush=True)
 
 
