@@ -119,11 +119,12 @@ __global__ void k_insert(const unsigned long long* __restrict__ keys, const uint
 template <int K, bool ORIG>
 __global__ __launch_bounds__(256) void k_knn(GridView g, const float* __restrict__ q, int64_t nq, int kq, int k,
                                               void* __restrict__ idx_out, int idx64, int exclude_self,
-                                              float* __restrict__ d2_out) {
+                                              float* __restrict__ d2_out, const int32_t* __restrict__ order) {
     const int64_t nb = gridDim.x;
     const int64_t b = xcd_block(blockIdx.x, nb);
-    const int64_t i = b * blockDim.x + threadIdx.x;
-    if (i >= nq) return;
+    const int64_t t = b * blockDim.x + threadIdx.x;
+    if (t >= nq) return;
+    const int64_t i = order ? (int64_t)order[t] : t;   // spatial order: a wave's queries share cells and L2 lines
     const Vec3 qi = v3(q[3 * i], q[3 * i + 1], q[3 * i + 2]);
     TopK<K> tk;
     knn_search<K, ORIG>(g, qi, tk);
@@ -141,9 +142,11 @@ __global__ __launch_bounds__(256) void k_knn(GridView g, const float* __restrict
     }
 }
 
-__global__ void k_nn1(GridView g, const float* __restrict__ q, int64_t nq, float* __restrict__ d2_out, int64_t* __restrict__ idx_out) {
-    const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    if (i >= nq) return;
+__global__ void k_nn1(GridView g, const float* __restrict__ q, int64_t nq, float* __restrict__ d2_out,
+                      int64_t* __restrict__ idx_out, const int32_t* __restrict__ order) {
+    const int64_t t = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (t >= nq) return;
+    const int64_t i = order ? (int64_t)order[t] : t;
     TopK<1> tk;
     knn_search<1, true>(g, v3(q[3 * i], q[3 * i + 1], q[3 * i + 2]), tk);
     if (d2_out) d2_out[i] = tk.d2(0);
@@ -201,13 +204,54 @@ int knn_cap(int k) {
     return -1;
 }
 
+// Queries in the caller's order are spatially random (a moved cloud in its input order): every lane of a wave then
+// reads its own cells and nothing is shared in L1/L2 (the 6 KB/query of the round-1 kNN(6) over 10M points).  Large
+// query sets are processed in the Morton order of the grid's lattice instead: keys, a radix sort of (key, index),
+// and the kernels read query order[t] and write row order[t].  Results are identical (per-query work only moves).
+struct QueryOrder {
+    int32_t* order = nullptr;
+    void* mem = nullptr;
+    hipStream_t st = nullptr;
+    ~QueryOrder() { if (mem) (void)hipFreeAsync(mem, st); }   // stream-ordered: after the kernels that read it
+};
+static constexpr int64_t kOrderMinQueries = 32768;
+static int query_order(const GridView& g, const float* q, int64_t nq, hipStream_t st, QueryOrder& qo) {
+    if (nq < kOrderMinQueries || nq >= (int64_t)INT32_MAX) return PCD_OK;
+    int maxd = std::max({g.dx, g.dy, g.dz, 2});
+    int bits = 0;
+    while ((1 << bits) < maxd) ++bits;
+    const unsigned end_bit = (unsigned)std::min(63, 3 * bits);
+    size_t tmp_bytes = 0;
+    unsigned long long *keys = nullptr, *keys2 = nullptr;
+    int32_t *vals = nullptr, *order = nullptr;
+    (void)rocprim::radix_sort_pairs(nullptr, tmp_bytes, keys, keys2, vals, order, (size_t)nq, 0u, end_bit, st);
+    const size_t off_k2 = (size_t)nq * 8, off_v = 2 * off_k2, off_o = off_v + (size_t)nq * 4,
+                 off_t = (off_o + (size_t)nq * 4 + 255) & ~(size_t)255;
+    if (hipMallocAsync(&qo.mem, off_t + tmp_bytes, st) != hipSuccess) return fail(PCD_ERR_OOM, "query order scratch");
+    qo.st = st;
+    char* base = static_cast<char*>(qo.mem);
+    keys = reinterpret_cast<unsigned long long*>(base);
+    keys2 = reinterpret_cast<unsigned long long*>(base + off_k2);
+    vals = reinterpret_cast<int32_t*>(base + off_v);
+    order = reinterpret_cast<int32_t*>(base + off_o);
+    hipLaunchKernelGGL(k_keys, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, st, q, nq, g.ox, g.oy, g.oz, g.inv_h, keys,
+                       vals);
+    if (rocprim::radix_sort_pairs(base + off_t, tmp_bytes, keys, keys2, vals, order, (size_t)nq, 0u, end_bit, st) !=
+        hipSuccess)
+        return fail(PCD_ERR_HIP, "query order: rocprim::radix_sort_pairs failed");
+    qo.order = order;
+    return PCD_OK;
+}
+
 template <bool ORIG>
 static int launch_knn(const GridView& g, const float* q, int64_t nq, int kq, int k, void* idx, int idx64,
                       int excl, float* d2, hipStream_t st) {
+    QueryOrder qo;
+    if (const int rc = query_order(g, q, nq, st, qo); rc != PCD_OK) return rc;
     const int cap = knn_cap(kq);
     const dim3 blk(256), grd((unsigned)cdiv(nq, 256));
 #define PCD_KNN_CASE(C) \
-    case C: hipLaunchKernelGGL((k_knn<C, ORIG>), grd, blk, 0, st, g, q, nq, kq, k, idx, idx64, excl, d2); break;
+    case C: hipLaunchKernelGGL((k_knn<C, ORIG>), grd, blk, 0, st, g, q, nq, kq, k, idx, idx64, excl, d2, qo.order); break;
     switch (cap) {
         PCD_KNN_CASE(1) PCD_KNN_CASE(4) PCD_KNN_CASE(8) PCD_KNN_CASE(13) PCD_KNN_CASE(16) PCD_KNN_CASE(32)
         PCD_KNN_CASE(64)
@@ -482,8 +526,10 @@ int pcd_nn_dist(const pcd_grid* g, const float* q, int64_t nq, float* d2_out, in
     PCD_CHECK_ARG(g != nullptr, "grid is null");
     if (nq == 0) return PCD_OK;
     PCD_CHECK_ARG(q != nullptr, "null query");
+    QueryOrder qo;
+    if (const int rc = query_order(g->view, q, nq, as_stream(stream), qo); rc != PCD_OK) return rc;
     hipLaunchKernelGGL(k_nn1, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, as_stream(stream), g->view, q, nq,
-                       d2_out, idx_out);
+                       d2_out, idx_out, qo.order);
     PCD_LAUNCH_CHECK();
     return PCD_OK;
 }

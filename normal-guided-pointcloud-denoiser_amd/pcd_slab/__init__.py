@@ -85,7 +85,9 @@ class SlabPlan:
 # ----------------------------------------------------------------------------------------------- transport
 class TorchTransport:
     """Halo exchange and scalar all-reduces over torch.distributed: NCCL (= RCCL on ROCm, over xGMI) moves device
-    tensors directly; gloo stages through host memory."""
+    tensors directly; gloo stages through host memory.  With NCCL, Work.wait() only makes the current (launch) stream
+    wait for the communication stream -- the exchanges stay stream-ordered and the host is not blocked; the halo
+    costs are measured per stage by SlabDenoiser.iterate_timed (fn_exchange, phases_with_exchange)."""
 
     def __init__(self, group=None):
         import torch.distributed as dist
@@ -206,7 +208,12 @@ class SlabDenoiser:
             snap_pos = self.t.broadcast_(snap_pos.contiguous().clone())
             snap_n = self.t.broadcast_(snap_n.contiguous().clone())
         if halo is None:
-            halo = default_halo(snap_pos, k_max)
+            # one rank grids the whole cloud for the estimate and broadcasts it (every rank planning from the same
+            # value; the others never build a grid over the global cloud)
+            h = torch.zeros(1, dtype=torch.float64, device=snap_pos.device)
+            if rank == 0:
+                h.fill_(default_halo(snap_pos, k_max))
+            halo = float(self.t.broadcast_(h)) if world > 1 else float(h)
         self.plan = SlabPlan.build(snap_pos, world, halo)
         plan = self.plan
         self.local = plan.local[rank]                           # global ids, ascending

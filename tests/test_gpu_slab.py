@@ -1,6 +1,6 @@
-"""Spatial slabs on the GPU: the staged HIP engine against the one-GPU fused loop, with one rank
-and with two ranks sharing the box's GPU over gloo (RCCL needs one GPU per rank; the 8-GPU RCCL run is the
-driver's bench)."""
+"""Spatial slabs on the GPU: the staged HIP engine against the one-GPU fused loop, with one rank,
+with two ranks sharing the box's GPU over gloo, and -- where at least two GPUs are visible -- two ranks on two GPUs
+over RCCL (backend "nccl"; skipped on a one-GPU box, the driver's 8-GPU bench exercises it at scale)."""
 import os
 import socket
 
@@ -26,11 +26,19 @@ def _d(pos):
     return 2 * float(Processor(Pointcloud(pos.clone())).meanEdgeLength())
 
 
-def _fused(pos, nrm, d):
+def _params(d, jacobi=False):
+    if not jacobi:
+        return nat.make_params(k=K, k_update=KU, d=d)
+    # the thesis driver's composition (PostProcessing.ipynb:1069-1090): Jacobi across classes + global clamp
+    ph = ((0, nat.STEP_FLAT, 1.0), (1, nat.STEP_FEATURE, 0.2), (2, nat.STEP_FEATURE, 1.0))
+    return nat.make_params(k=K, k_update=KU, d=d * 20000, phases=ph, jacobi=True, clamp_global=d)
+
+
+def _fused(pos, nrm, d, jacobi=False):
     g = nat.Grid(pos, k_hint=K)
     fd = nat.FusedDenoiser(g, max(K, KU))
     fd.load(pos, nrm)
-    fd.iterate(nat.make_params(k=K, k_update=KU, d=d), ITERS)
+    fd.iterate(_params(d, jacobi), ITERS)
     p, n = torch.empty_like(pos), torch.empty_like(nrm)
     fd.store(p, n)
     return p.cpu().numpy(), n.cpu().numpy()
@@ -55,19 +63,22 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_path, cloud_path, d):
+def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", rank if backend == "nccl" else 0)
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        dev = torch.device("cuda", 0)
-        torch.cuda.set_device(dev)
         c = np.load(cloud_path)
         pos, nrm = torch.from_numpy(c["pos"]).to(dev), torch.from_numpy(c["n"]).to(dev)
         tr = TorchTransport()
         sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K)
-        sd.iterate(nat.make_params(k=K, k_update=KU, d=d), ITERS)
+        sd.iterate(_params(d, jacobi), ITERS)
         sd.check()
         p, n = gather_global(sd.owned_state(), pos.size(0), tr)
         if rank == 0:
@@ -89,6 +100,54 @@ def test_hip_slab_world2_matches_one_gpu(gpu, tmp_path):
     rp, rn = _fused(pos, nrm, d)
     bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
     # same kernels and tie-breaks; only the f64 summation order of the global flat centre differs
+    np.testing.assert_allclose(res["pos"], rp, rtol=0, atol=1e-6 * bbox)
+    np.testing.assert_allclose(res["n"], rn, rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_hip_slab_world1_jacobi_is_the_fused_loop(gpu):
+    """The Jacobi-across-classes mode with the global clamp through the staged engine (one position refresh per
+    iteration instead of one per phase): bit-identical to the fused loop at world 1."""
+    pos, nrm = _cloud(gpu)
+    d = _d(pos)
+    sd = SlabDenoiser(pos, nrm, max(K, KU), transport=LocalTransport(), k_hint=K)
+    sd.iterate(_params(d, True), ITERS)
+    p, n = gather_global(sd.owned_state(), pos.size(0), sd.t)
+    rp, rn = _fused(pos, nrm, d, True)
+    np.testing.assert_array_equal(p.cpu().numpy(), rp)
+    np.testing.assert_array_equal(n.cpu().numpy(), rn)
+
+
+@pytest.mark.gpu
+def test_hip_slab_world2_jacobi_matches_one_gpu(gpu, tmp_path):
+    import torch.multiprocessing as mp
+    pos, nrm = _cloud(gpu)
+    d = _d(pos)
+    out, cloud = str(tmp_path / "slab2j.npz"), str(tmp_path / "cloud.npz")
+    np.savez(cloud, pos=pos.cpu().numpy(), n=nrm.cpu().numpy())
+    mp.spawn(_worker, args=(2, _free_port(), out, cloud, d, "gloo", True), nprocs=2, join=True)
+    res = np.load(out)
+    rp, rn = _fused(pos, nrm, d, True)
+    bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
+    np.testing.assert_allclose(res["pos"], rp, rtol=0, atol=1e-6 * bbox)
+    np.testing.assert_allclose(res["n"], rn, rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_hip_slab_world2_rccl_two_gpus(gpu, tmp_path):
+    """Two ranks on two GPUs over RCCL (the bench's multi-GPU transport); needs >= 2 visible GPUs."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (RCCL ranks cannot share one device)")
+    import torch.multiprocessing as mp
+    pos, nrm = _cloud(gpu)
+    d = _d(pos)
+    out, cloud = str(tmp_path / "slab2r.npz"), str(tmp_path / "cloud.npz")
+    np.savez(cloud, pos=pos.cpu().numpy(), n=nrm.cpu().numpy())
+    mp.spawn(_worker, args=(2, _free_port(), out, cloud, d, "nccl"), nprocs=2, join=True)
+    res = np.load(out)
+    assert int(res["halo"]) > 0
+    rp, rn = _fused(pos, nrm, d)
+    bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
     np.testing.assert_allclose(res["pos"], rp, rtol=0, atol=1e-6 * bbox)
     np.testing.assert_allclose(res["n"], rn, rtol=0, atol=1e-5)
 
