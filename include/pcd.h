@@ -209,6 +209,10 @@ int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n
 /* Device error word -> status: PCD_ERR_STATE if a kNN list held an invalid entry or (spatial slabs) a query's
  * k-ball left the coverage box.  Synchronises `stream`.  store() calls it. */
 int pcd_denoiser_check(pcd_denoiser* dn, void* stream);
+/* The kNN list the last K1 stage stored (the snapshot's `cols` nearest of each point's current position, in
+ * (distance, index) order = getKNNSelection's columns, Selector.py:235-246), in caller order with ORIGINAL snapshot
+ * indices: out int64 [N][cols], cols <= the stored list length (max(k, k_update) of the last iteration). */
+int pcd_denoiser_lists(pcd_denoiser* dn, int64_t* out, int cols, void* stream);
 
 /* ---- spatial slabs (multi-GPU): the same loop over a rank's own points with a halo ----
  * The grid holds the rank's points plus halo snapshot points owned by other ranks.  Only the ACTIVE rows are

@@ -276,11 +276,15 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
             int below = 0;
 #pragma unroll
             for (int t = 0; t < KA; ++t) {
-                const uint32_t rt = min(r[t], (uint32_t)(N - 1));
+                const bool slot = r[t] < (uint32_t)N;   // -1: unused slot of a partial anchor set
+                const uint32_t rt = slot ? r[t] : 0u;
                 s_r[t * kAnchorBS + threadIdx.x] = rt;
-                const float d2 = dist2(vi, g.pts[rt]);
+                const float d2r = dist2(vi, g.pts[rt]);   // unconditional load: all KA gathers stay in flight
+                const float d2 = slot ? d2r : __int_as_float(0x7F800000);
                 below += d2 < T ? 1 : 0;
-                c[t] = ((uint32_t)fminf(d2 * S, 67108863.f) << 6) | (uint32_t)t;
+                // clamp below 2^26 in fp32 (2^26 - 1 rounds UP to 2^26, which would wrap to 0 after the shift);
+                // only unused slots (infinite distance) reach it
+                c[t] = ((uint32_t)fminf(d2 * S, 67108860.f) << 6) | (uint32_t)t;
             }
             bitonic_sort<KA>(c);
             bool ok = below >= kstore;
@@ -301,19 +305,12 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
                                                  // spatial order, so the waves in flight on an XCD share its L2
 }
 
-// NVT1 + eigh + VU smoothing over the stored lists (lane per active row); checks every list entry and, for
-// spatial slabs, that the kstore-ball stays inside the local snapshot.
-template <int K>
-__global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
-                                               const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
-                                               int kstore, float rho, float tau, float damp, Cover cov,
-                                               float4* __restrict__ fn, int* __restrict__ err, int win) {
-    __shared__ float4 s_pos[kWinRows], s_nrm[kWinRows];
-    const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
-    const int64_t lo = stage_window(pos, nrm, N, rm(b0), s_pos, s_nrm, win);
-    const int64_t t0 = b0 + threadIdx.x;
-    if (t0 >= rm.nq) return;
-    const int64_t i = rm(t0);
+// NVT1 + eigh + VU smoothing over the stored lists (lane per row); checks every list entry and, for spatial slabs,
+// that the kstore-ball stays inside the local snapshot.
+template <int K, class P, class Nr>
+__device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
+                      const int32_t* __restrict__ idx, int64_t N, int64_t i, int k, int kstore, float rho, float tau,
+                      float damp, const Cover& cov, float4* __restrict__ fn, int* __restrict__ err, P rp, Nr rn) {
     const float4 p4 = pos[i];
     const Vec3 vi = v3(p4.x, p4.y, p4.z);
     int l[K];
@@ -331,13 +328,43 @@ __global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restri
             if (t == kstore - 1) dk = dist2(vi, g.pts[l[t]]);
         if (!cov.holds(vi, dk)) atomicOr(err, 2);
     }
-    const Sym3 T = nvt_tensor<K>(WinRows<>{pos, s_pos, lo}, WinRows<>{nrm, s_nrm, lo}, vi, k, RegNb32{l}, rho,
-                                 ColNbSafe{idx, N, i});
+    const Sym3 T = nvt_tensor<K>(rp, rn, vi, k, RegNb32{l}, rho, ColNbSafe{idx, N, i});
     float w[3], V[3][3];
     eigh3(T, w, V);
     const float4 n4 = nrm[i];
     const Vec3 f = vu_smooth(w, V, v3(n4.x, n4.y, n4.z), tau, damp);
     __builtin_nontemporal_store(v4f{f.x, f.y, f.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
+}
+
+// Every active row, or (skip != null) every active row t with skip[t] == 0: the rows the anchor test certified,
+// run on a side stream while the re-anchoring search works on the others (pcd_denoiser::side).
+template <int K>
+__global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
+                                               const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
+                                               int kstore, float rho, float tau, float damp, Cover cov,
+                                               float4* __restrict__ fn, int* __restrict__ err, int win,
+                                               const uint8_t* __restrict__ skip) {
+    __shared__ float4 s_pos[kWinRows], s_nrm[kWinRows];
+    const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
+    const int64_t lo = stage_window(pos, nrm, N, rm(b0), s_pos, s_nrm, win);
+    const int64_t t0 = b0 + threadIdx.x;
+    if (t0 >= rm.nq) return;
+    if (skip && skip[t0]) return;
+    nvt1_row<K>(g, pos, nrm, idx, N, rm(t0), k, kstore, rho, tau, damp, cov, fn, err, WinRows<>{pos, s_pos, lo},
+                WinRows<>{nrm, s_nrm, lo});
+}
+
+// The rows of list[0 .. *cnt) (the re-anchored rows, spatially sparse: no LDS window), grid-stride.
+template <int K>
+__global__ __launch_bounds__(256) void k_nvt1_list(GridView g, const float4* __restrict__ pos,
+                                                    const float4* __restrict__ nrm, const int32_t* __restrict__ idx,
+                                                    int64_t N, int k, int kstore, float rho, float tau, float damp,
+                                                    Cover cov, float4* __restrict__ fn, int* __restrict__ err,
+                                                    const int32_t* __restrict__ list, const unsigned* __restrict__ cnt) {
+    const int64_t n = (int64_t)*cnt;
+    for (int64_t t = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x; t < n;
+         t += (int64_t)gridDim.x * blockDim.x)
+        nvt1_row<K>(g, pos, nrm, idx, N, list[t], k, kstore, rho, tau, damp, cov, fn, err, Rows4{pos}, Rows4{nrm});
 }
 
 // Re-anchor: the exact KA nearest at the current position, one query per WAVE (pcd_wknn.h), capped by the old
@@ -369,7 +396,9 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
         unsigned long long cap = kInfKey;
         if (!DENSE) {
             const float4 a = anc[i];
-            if (a.w >= 0.f) cap = anchor_cap(q, a);
+            // (D + |q - a|)² bounds the KA-th key at q only for a FULL anchor set (KA points within D of a); a partial
+            // set (fewer points within its radius, unused slots -1) gives no such bound
+            if (a.w >= 0.f && alist[(int64_t)(KA - 1) * N + i] >= 0) cap = anchor_cap(q, a);
         }
         const unsigned long long top = wave_knn<KA>(g, q, cap, s_buf[wv], &s_cells[wv], lane);
         // a slot without a finite candidate (non-finite query, fewer than KA points) is never stored as an index:
@@ -583,6 +612,18 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     store4(pout, i, o);
 }
 
+// pcd_denoiser_lists: column-major sorted-order lists -> caller rows of original indices
+__global__ void k_lists(const int32_t* __restrict__ idx, const int32_t* __restrict__ perm, int64_t N, int cols,
+                        int64_t* __restrict__ out) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    const int64_t i = perm[r];
+    for (int t = 0; t < cols; ++t) {
+        const int32_t j = idx[(int64_t)t * N + r];
+        out[i * cols + t] = (uint32_t)j < (uint64_t)N ? (int64_t)perm[j] : -1;
+    }
+}
+
 // halo exchange: rows of one state field <-> a packed float4 buffer
 __global__ void k_pack(const float4* __restrict__ f, const int32_t* __restrict__ rows, int64_t n, float4* __restrict__ out) {
     const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -614,6 +655,7 @@ struct pcd_denoiser {
     int64_t n_rows = 0;
     Cover cov{{1.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};  // disabled
     int seed_cols = 0;            // columns of idx holding a valid kNN list of the snapshot (0: none yet)
+    int list_cols = 0;            // columns the last K1 stage stored (pcd_denoiser_lists)
     bool seeding = true;          // use the stored list as an acceptance cap (pcd_denoiser_set_seeding)
     // anchored kNN (list cap <= 32): anchors + their 2K-lists, the redo list of queries that failed the test
     float4* anc = nullptr;
@@ -625,6 +667,8 @@ struct pcd_denoiser {
     void* sel_tmp = nullptr;      // rocprim::select scratch
     size_t sel_bytes = 0;
     int anchor_ka = 0;            // KA of the stored anchors (0: none)
+    hipStream_t side = nullptr;   // NVT1 of the certified rows, concurrent with the re-anchoring search
+    hipEvent_t fork = nullptr, join = nullptr;
     int64_t last_dense = -1;      // rows of the last anchored stage when it re-anchored every row, else -1
     bool anchoring = true;        // anchored kNN for seeded searches (pcd_denoiser_set_anchoring)
     int windows = 1;              // LDS row windows in NVT1 / NVT2 / the flat phase (pcd_denoiser_set_windows)
@@ -694,6 +738,9 @@ static int select_rows(pcd_denoiser* dn, const RowMap& rm, int32_t* list, unsign
 #ifndef PCD_RQ_GRID
 #define PCD_RQ_GRID 4096
 #endif
+#ifndef PCD_NVT1_OVERLAP
+#define PCD_NVT1_OVERLAP 0   // measured: the side-stream NVT1 slows the re-anchoring more than it hides
+#endif
 static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int K, hipStream_t st,
                              hipEvent_t* ev) {
     const int64_t N = dn->n;
@@ -722,6 +769,16 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     const dim3 grd_wave((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), PCD_REDO_GRID));
     const dim3 grd_anc((unsigned)cdiv(rm.nq, kAnchorBS));
     int rc = PCD_OK;
+    // Dense (no anchors): every row is re-anchored, then NVT1 runs over all rows.  Seeded: the anchor test, then
+    // NVT1 of the certified rows on the side stream while this stream re-anchors the others (latency-bound wave
+    // searches beside VALU-bound lane work), then NVT1 of the re-anchored rows, then the join.
+    const bool overlap = !dense && PCD_NVT1_OVERLAP;
+    if (overlap && !dn->side) {
+        PCD_HIP(hipStreamCreateWithFlags(&dn->side, hipStreamNonBlocking));
+        PCD_HIP(hipEventCreateWithFlags(&dn->fork, hipEventDisableTiming));
+        PCD_HIP(hipEventCreateWithFlags(&dn->join, hipEventDisableTiming));
+    }
+    const dim3 grd_list((unsigned)std::min<int64_t>(cdiv(rm.nq, 256), 1024));
 #define PCD_K1A(C)                                                                                                     \
     case C:                                                                                                            \
         if (dense) {                                                                                                   \
@@ -732,6 +789,13 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
             hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd_anc, dim3(kAnchorBS), 0, st, gv, P, N, rm, kstore,        \
                                dn->anc, dn->alist, dn->idx, dn->fail);                                                 \
             if ((rc = select_rows(dn, rm, dn->redo, redo_cnt, st)) != PCD_OK) return rc;                               \
+            if (overlap) {                                                                                             \
+                PCD_HIP(hipEventRecord(dn->fork, st));                                                                 \
+                PCD_HIP(hipStreamWaitEvent(dn->side, dn->fork, 0));                                                    \
+                hipLaunchKernelGGL((k_nvt1<C>), grd, blk, 0, dn->side, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,   \
+                                   p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, dn->fail);          \
+                PCD_HIP(hipEventRecord(dn->join, dn->side));                                                           \
+            }                                                                                                          \
             if (ev) PCD_HIP(hipEventRecord(ev[1], st));                                                                \
             hipLaunchKernelGGL((k_knn_requery<2 * C, false>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, 0.f, dn->anc,  \
                                dn->alist, dn->idx, dn->redo, redo_cnt, dn->spill, spill_cnt);                         \
@@ -740,8 +804,14 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
         hipLaunchKernelGGL((k_knn_redo_wave<2 * C, false>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,       \
                            dn->alist, dn->idx, dn->spill, spill_cnt, dn->err);                                         \
         if (ev) PCD_HIP(hipEventRecord(ev[3], st));                                                                    \
-        hipLaunchKernelGGL((k_nvt1<C>), grd, blk, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore, p->rho, p->tau, \
-                           p->damp, dn->cov, dn->fn, dn->err, dn->windows);                                          \
+        if (overlap) {                                                                                                 \
+            hipLaunchKernelGGL((k_nvt1_list<C>), grd_list, blk, 0, st, gv, P, dn->nrm, dn->idx, N, p->k, kstore,       \
+                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->redo, redo_cnt);                 \
+            PCD_HIP(hipStreamWaitEvent(st, dn->join, 0));                                                              \
+        } else {                                                                                                       \
+            hipLaunchKernelGGL((k_nvt1<C>), grd, blk, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore, p->rho,     \
+                               p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, nullptr);                       \
+        }                                                                                                              \
         break;
     switch (K) {
         PCD_K1A(8) PCD_K1A(16) PCD_K1A(32)
@@ -750,7 +820,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
 #undef PCD_K1A
     PCD_LAUNCH_CHECK();
     dn->anchor_ka = KA;
-    dn->seed_cols = kstore;
+    dn->seed_cols = dn->list_cols = kstore;
     return PCD_OK;
 }
 
@@ -778,7 +848,7 @@ static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t s
     }
 #undef PCD_K1
     PCD_LAUNCH_CHECK();
-    dn->seed_cols = kstore;
+    dn->seed_cols = dn->list_cols = kstore;
     return PCD_OK;
 }
 
@@ -928,6 +998,9 @@ int pcd_denoiser_destroy(pcd_denoiser* dn) {
     (void)hipFree(dn->red); (void)hipFree(dn->gscal); (void)hipFree(dn->err);
     (void)hipFree(dn->anc); (void)hipFree(dn->alist); (void)hipFree(dn->redo); (void)hipFree(dn->spill);
     (void)hipFree(dn->rqs); (void)hipFree(dn->fail); (void)hipFree(dn->sel_tmp);
+    if (dn->side) (void)hipStreamDestroy(dn->side);
+    if (dn->fork) (void)hipEventDestroy(dn->fork);
+    if (dn->join) (void)hipEventDestroy(dn->join);
     for (auto e : dn->ev) (void)hipEventDestroy(e);
     delete dn;
     return PCD_OK;
@@ -1020,6 +1093,15 @@ int pcd_denoiser_check(pcd_denoiser* dn, void* stream) {
     if (err & 1) return fail(PCD_ERR_STATE, "pcd_denoiser: the kNN kernel produced an invalid neighbour index");
     if (err & 2)
         return fail(PCD_ERR_STATE, "pcd_denoiser: a k-neighbourhood reaches past the local snapshot (halo too thin)");
+    return PCD_OK;
+}
+
+int pcd_denoiser_lists(pcd_denoiser* dn, int64_t* out, int cols, void* stream) {
+    PCD_CHECK_ARG(dn && out, "null argument");
+    PCD_CHECK_ARG(dn->iterated && cols >= 1 && cols <= dn->list_cols, "cols must be in [1, stored list length]");
+    hipLaunchKernelGGL(k_lists, dim3((unsigned)cdiv(dn->n, 256)), dim3(256), 0, as_stream(stream), dn->idx,
+                       dn->g->perm, dn->n, cols, out);
+    PCD_LAUNCH_CHECK();
     return PCD_OK;
 }
 

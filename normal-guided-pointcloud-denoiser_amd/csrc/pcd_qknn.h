@@ -316,6 +316,9 @@ PCD_DEV bool rq_scan_box(const GridView& g, Vec3 q, const int lo[3], const int h
 // rows spilled to the exact-key wave search (= length of the spill list).
 struct RqStats { unsigned redo_cnt, spill_cnt, spill_big, spill_amb; };
 
+#ifndef PCD_RQ_RSCALE
+#define PCD_RQ_RSCALE 1.1f   // re-anchoring radius / the old anchor's D
+#endif
 #ifndef PCD_RQ_OCC
 #define PCD_RQ_OCC 8
 #endif
@@ -342,34 +345,35 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
         const int64_t i = __builtin_amdgcn_readfirstlane(DENSE ? (int)rm(t0) : list[t0]);
         const float4 p4 = pos[i];
         const Vec3 q = v3(p4.x, p4.y, p4.z);
-        unsigned long long cap;
-        float r_dense = 0.f;
+        // The search radius r: DENSE from the occupancy of the query's cell, else from the old anchor's D (the local
+        // KA-th distance; the cap (D + |q - a|)^2 that bounds the KA-th key at q is ~2x the area to scan).  The new
+        // anchor set is the KA nearest within r, or -- when fewer than KA points lie within r -- ALL of them, with
+        // D = r: every other snapshot point is then farther than r, which is all the anchor test needs.
+        float r_s;
         if (DENSE) {
             const int cx = min(max(cell_coord(q.x, g.ox, g.inv_h), 0), g.dx - 1);
             const int cy = min(max(cell_coord(q.y, g.oy, g.inv_h), 0), g.dy - 1);
             const int cz = min(max(cell_coord(q.z, g.oz, g.inv_h), 0), g.dz - 1);
             uint32_t s = 0, e = 0;
             const int n = cell_range(g, cx, cy, cz, s, e) ? (int)(e - s) : 1;
-            r_dense = r_scale * g.h * cbrtf(16.f / (float)n);
-            cap = ((unsigned long long)__float_as_uint(r_dense * r_dense) << 32) | 0xFFFFFFFFull;
+            r_s = r_scale * g.h * cbrtf(16.f / (float)n);
         } else {
             const float4 a = anc[i];
-            if (!(a.w >= 0.f)) {                      // no anchor: the wave search grows its own box
+            if (!(a.w > 0.f)) {                       // no anchor: the wave search grows its own box
                 if (lane == 0) spill[atomicAdd(spill_cnt, 1u)] = (int32_t)i;
                 continue;
             }
-            cap = anchor_cap(q, a);
+            r_s = a.w * PCD_RQ_RSCALE;
         }
+        unsigned long long cap = 0;
         int cnt = 0;
         bool big = false, ok = false;
-        // dense: a radius guess holding fewer than KA points is widened (x 1.6, twice) before the query spills
+        // a radius holding at most kstore points is widened (x 1.6, twice) before the query spills
 #pragma unroll 1
-        for (int attempt = 0; attempt < (DENSE ? 3 : 1); ++attempt) {
-            if (attempt > 0) {
-                r_dense *= 1.6f;
-                cap = ((unsigned long long)__float_as_uint(r_dense * r_dense) << 32) | 0xFFFFFFFFull;
-            }
-            const float rr = sqrtf(__uint_as_float((unsigned)(cap >> 32))) * 1.0001f + 1e-30f;
+        for (int attempt = 0; attempt < 3; ++attempt) {
+            if (attempt > 0) r_s *= 1.6f;
+            cap = ((unsigned long long)__float_as_uint(r_s * r_s) << 32) | 0xFFFFFFFFull;
+            const float rr = r_s * 1.0001f + 1e-30f;
             int lo[3], hi[3];
             cell_box(g, q, rr, lo, hi);
             cnt = 0;
@@ -377,10 +381,11 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
             big = nbox > kRqMaxCells;
             if (big) break;
             const bool clean = rq_scan_box<KA>(g, q, lo, hi, cap, buf, cnt, &s_cells[wv], lane);
-            ok = clean && cnt >= KA;
+            ok = clean && cnt > kstore;
             if (ok || !clean) break;
             wave_sync();
         }
+        const bool partial = cnt < KA;               // (after a buffer cut cnt == KA)
         uint32_t k = 0xFFFFFFFFu;
         if (ok) {
             uint32_t after;
@@ -390,7 +395,7 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
             ok = order_exact(k, after, kstore, lane);
             const uint32_t kK = KA < 64 ? (uint32_t)__shfl((int)k, KA < 64 ? KA : 0) : after;  // element KA
             const uint32_t kK1 = (uint32_t)__shfl((int)k, KA - 1);
-            ok = ok && (cnt == KA || (kK >> 8) != (kK1 >> 8));
+            ok = ok && (cnt <= KA || (kK >> 8) != (kK1 >> 8));
         }
         if (!ok) {
             wave_sync();
@@ -400,8 +405,10 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
             }
             continue;
         }
-        const unsigned long long mine = lane < KA ? buf[k & 255u] : 0ull;
-        const int32_t r = (int32_t)(uint32_t)(mine & 0xFFFFFFFFull);
+        const bool have = lane < KA && lane < cnt;
+        const unsigned long long mine = have ? buf[k & 255u] : 0ull;
+        // unused slots of a partial set hold -1 (the anchor test gives them an infinite distance)
+        const int32_t r = have ? (int32_t)(uint32_t)(mine & 0xFFFFFFFFull) : -1;
 #if defined(PCD_EXP_RQ_WRITE) && PCD_EXP_RQ_WRITE == 1      // timing experiment: no list writes (results wrong)
         if (r == -12345) alist[i] = r;
 #elif defined(PCD_EXP_RQ_WRITE) && PCD_EXP_RQ_WRITE == 2    // timing experiment: contiguous writes (results wrong)
@@ -410,9 +417,11 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
         if (lane < KA) alist[(int64_t)lane * N + i] = r;
         if (lane < kstore) idx[(int64_t)lane * N + i] = r;
 #endif
-        // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless)
-        const unsigned long long mx = wave_max_u64(lane < KA ? mine : 0ull);
-        if (lane == 0) anc[i] = make_float4(q.x, q.y, q.z, sqrtf(__uint_as_float((unsigned)(mx >> 32))));
+        // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
+        // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))
+        const unsigned long long mx = wave_max_u64(mine);
+        const float D = partial ? r_s * (1.f - 1e-6f) : sqrtf(__uint_as_float((unsigned)(mx >> 32)));
+        if (lane == 0) anc[i] = make_float4(q.x, q.y, q.z, D);
         wave_sync();                                  // buf is free for the next query
     }
 }

@@ -80,6 +80,7 @@ _SIGS = {
     "pcd_denoiser_anchor_stats": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_denoiser_tile_stats": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_denoiser_check": (c_int, [c_void_p, c_void_p]),
+    "pcd_denoiser_lists": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "pcd_denoiser_set_rows": (c_int, [c_void_p, c_void_p, c_int64]),
     "pcd_denoiser_set_coverage": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_denoiser_stage": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
@@ -271,6 +272,12 @@ class FusedDenoiser:
     def store(self, pos=None, n=None, classes=None, edge_vectors=None):
         check(lib().pcd_denoiser_store(self.handle, ptr(pos), ptr(n), ptr(classes), ptr(edge_vectors),
                                        c_void_p(stream_ptr())), "pcd_denoiser_store")
+
+    def lists(self, cols: int) -> torch.Tensor:
+        """The kNN lists of the last iteration (original indices, caller order): int64 [N, cols]."""
+        out = torch.empty((self.grid.n, int(cols)), dtype=torch.int64, device=device())
+        check(lib().pcd_denoiser_lists(self.handle, ptr(out), int(cols), c_void_p(stream_ptr())), "pcd_denoiser_lists")
+        return out
 
     def set_seeding(self, enable=True):
         check(lib().pcd_denoiser_set_seeding(self.handle, int(bool(enable))), "pcd_denoiser_set_seeding")

@@ -5,6 +5,6 @@ set -o pipefail
 for v in "$@"; do
   if [ "$v" = cur ]; then lib=$PWD/normal-guided-pointcloud-denoiser_amd/libpcd.so
   else lib=$PWD/normal-guided-pointcloud-denoiser_amd/libpcd_$v.so; fi
-  out=$(PCD_LIB=$lib timeout -k 10 200 python bench.py --no-cpu-baseline 2>/dev/null | grep '^{') || { echo "$v failed"; exit 1; }
+  out=$(PCD_LIB=$lib timeout -k 10 200 python bench.py --no-cpu-baseline --no-ten --steps 20 --warmup 5 2>/dev/null | grep '^{') || { echo "$v failed"; exit 1; }
   echo "$out" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', d['ms_per_step'], d['value'], d['kernel_ms'])"
 done
