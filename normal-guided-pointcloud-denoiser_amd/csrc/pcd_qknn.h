@@ -1,5 +1,5 @@
-// Re-anchoring search of the anchored kNN (denoise.hip): the exact KA nearest snapshot points of a moved query,
-// one query per wave, lean enough for 8 waves per SIMD.
+// Re-anchoring search of the anchored kNN (denoise.hip): the exact KA nearest snapshot points of a moved query
+// within a radius, one query per group of W lanes (two per wave at W = 32), lean enough for 8 waves per SIMD.
 //
 // The search is the one of pcd_wknn.h (cap box -> brick probes -> flattened candidate rows -> ballot-appended
 // survivors below the acceptance cap), re-cut for occupancy and VALU:
@@ -27,20 +27,41 @@ PCD_DEV unsigned long long anchor_cap(Vec3 q, float4 a) {
     return ((unsigned long long)__float_as_uint(R2) << 32) | 0xFFFFFFFFull;
 }
 
-// Ascending bitonic sort of the 64*M 32-bit keys v[s] (element e = s*64 + lane) across the wave.
-template <int M>
-PCD_DEV void wave_bitonic_sort32(uint32_t (&v)[M], int lane) {
-    constexpr int NT = 64 * M;
+// Lane groups: W = 64 (one query per wave) or W = 32 (two queries per wave, one per half).  The search is a chain
+// of dependent memory round trips (query -> brick probes -> brick blocks -> candidate rows) with little VALU in
+// between (12 % VALU-active, 68 % of wave cycles waiting at 8 waves/SIMD), so two queries per wave keep twice as many
+// chains in flight for the same wave slots; the shuffles below stay inside a group (width-W shuffles) and the
+// ballots are masked to the group's bits.
+template <int W>
+struct LaneGrp {
+    int lane, hl, base;        // hl: lane inside the group; base: the group's first lane
+    PCD_DEV LaneGrp(int l) : lane(l), hl(l & (W - 1)), base(l & ~(W - 1)) {}
+    PCD_DEV unsigned long long bits(unsigned long long m) const {
+        return W == 64 ? m : (m >> base) & 0xFFFFFFFFull;
+    }
+    PCD_DEV unsigned long long ballot(bool p) const { return bits(__ballot(p)); }
+    PCD_DEV bool any(bool p) const { return ballot(p) != 0ull; }
+    PCD_DEV int below() const { return hl; }
+    PCD_DEV uint32_t bcast(uint32_t v, int src) const { return (uint32_t)__shfl((int)v, src, W); }
+    PCD_DEV unsigned long long bcast64(unsigned long long v, int src) const {
+        return (unsigned long long)bcast((uint32_t)v, src) | ((unsigned long long)bcast((uint32_t)(v >> 32), src) << 32);
+    }
+};
+
+// Ascending bitonic sort of the W*M 32-bit keys v[s] (element e = s*W + hl) across the group.
+template <int W, int M>
+PCD_DEV void grp_bitonic_sort32(uint32_t (&v)[M], int hl) {
+    constexpr int NT = W * M;
 #pragma unroll
     for (int size = 2; size <= NT; size <<= 1) {
 #pragma unroll
         for (int stride = size / 2; stride > 0; stride >>= 1) {
-            if (stride >= 64) {
-                const int ss = stride / 64;
+            if (stride >= W) {
+                const int ss = stride / W;
 #pragma unroll
                 for (int s = 0; s < M; ++s) {
                     if ((s & ss) == 0) {
-                        const bool asc = ((s * 64 + lane) & size) == 0;
+                        const bool asc = ((s * W + hl) & size) == 0;
                         const uint32_t a = v[s], b = v[s + ss];
                         const uint32_t mn = min(a, b), mx = max(a, b);
                         v[s] = asc ? mn : mx;
@@ -48,11 +69,11 @@ PCD_DEV void wave_bitonic_sort32(uint32_t (&v)[M], int lane) {
                     }
                 }
             } else {
-                const bool lower = (lane & stride) == 0;
+                const bool lower = (hl & stride) == 0;
 #pragma unroll
                 for (int s = 0; s < M; ++s) {
-                    const bool asc = ((s * 64 + lane) & size) == 0;
-                    const uint32_t o = (uint32_t)__shfl_xor((int)v[s], stride);
+                    const bool asc = ((s * W + hl) & size) == 0;
+                    const uint32_t o = (uint32_t)__shfl_xor((int)v[s], stride, W);
                     v[s] = (lower == asc) ? min(o, v[s]) : max(o, v[s]);
                 }
             }
@@ -60,9 +81,22 @@ PCD_DEV void wave_bitonic_sort32(uint32_t (&v)[M], int lane) {
     }
 }
 
-// The survivors buf[0..cnt) ordered by quantised 32-bit keys (cnt <= kWaveSurv): lane t returns element t
-// (0xFFFFFFFF past cnt) and the element after the last lane's (for the boundary checks of a full first slot).
-PCD_DEV uint32_t wave_order32(const unsigned long long* buf, int cnt, float capd2, int lane, uint32_t& after63) {
+// Survivors per group: room for a cut to KA = 64 plus one round of appends (W * kRqRows).
+template <int W> struct RqSurv { static constexpr int n = W == 64 ? 256 : 192; };
+
+// The quantised order of the survivors buf[0..cnt) (cnt <= RqSurv): element e lives in slot e / W of lane e % W;
+// o.s0 / o.s1 = this lane's elements hl and W + hl (0xFFFFFFFF past cnt), o.at(e) broadcasts element e.
+template <int W>
+struct GrpOrder {
+    uint32_t s0, s1, s2_0;     // slot 0, slot 1 of this lane; element 2W (slot 2, lane 0)
+    const LaneGrp<W>* g;
+    PCD_DEV uint32_t at(int e) const {   // e < 2W + 1
+        if (e >= 2 * W) return s2_0;
+        return e < W ? g->bcast(s0, e) : g->bcast(s1, e - W);
+    }
+};
+template <int W>
+PCD_DEV GrpOrder<W> grp_order32(const unsigned long long* buf, int cnt, float capd2, const LaneGrp<W>& g) {
     wave_sync();
     const float S = 16777216.f / fmaxf(capd2, 1e-30f);
     auto k32 = [&](int e) -> uint32_t {
@@ -70,66 +104,69 @@ PCD_DEV uint32_t wave_order32(const unsigned long long* buf, int cnt, float capd
         const float d2 = __uint_as_float((uint32_t)(buf[e] >> 32));
         return ((uint32_t)fminf(d2 * S, 16777214.f) << 8) | (uint32_t)e;
     };
-    uint32_t top;
-    if (cnt <= 64) {
-        uint32_t v[1] = {k32(lane)};
-        wave_bitonic_sort32<1>(v, lane);
-        top = v[0];
-        after63 = 0xFFFFFFFFu;
-    } else if (cnt <= 128) {
-        uint32_t v[2] = {k32(lane), k32(64 + lane)};
-        wave_bitonic_sort32<2>(v, lane);
-        top = v[0];
-        after63 = (uint32_t)__shfl((int)v[1], 0);
-    } else {
-        uint32_t v[4] = {k32(lane), k32(64 + lane), k32(128 + lane), k32(192 + lane)};
-        wave_bitonic_sort32<4>(v, lane);
-        top = v[0];
-        after63 = (uint32_t)__shfl((int)v[1], 0);
+    const int hl = g.hl;
+    GrpOrder<W> o{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, &g};
+    if (cnt <= W) {
+        uint32_t v[1] = {k32(hl)};
+        grp_bitonic_sort32<W, 1>(v, hl);
+        o.s0 = v[0];
+    } else if (cnt <= 2 * W) {
+        uint32_t v[2] = {k32(hl), k32(W + hl)};
+        grp_bitonic_sort32<W, 2>(v, hl);
+        o.s0 = v[0]; o.s1 = v[1];
+    } else {                                 // cnt <= 4W (callers spill a larger set that did not shrink)
+        uint32_t v[4] = {k32(hl), k32(W + hl), k32(2 * W + hl), k32(3 * W + hl)};
+        grp_bitonic_sort32<W, 4>(v, hl);
+        o.s0 = v[0]; o.s1 = v[1]; o.s2_0 = g.bcast(v[2], 0);
     }
-    return top;
+    return o;
 }
 
 // Do the first n elements of the quantised order hold their exact order and the set boundary after element
 // n-1?  Exact iff every quantised value among elements 0..n (n+1 elements) is distinct, i.e. no two neighbours
-// in 0..n share one (a pad compares larger than every real key).  n <= 64.
-PCD_DEV bool order_exact(uint32_t k, uint32_t after63, int n, int lane) {
-    const uint32_t nxt = lane == 63 ? after63 : (uint32_t)__shfl_down((int)k, 1);
-    const bool tie = lane < n && (k >> 8) == (nxt >> 8) && k != 0xFFFFFFFFu;
-    return !__any(tie);
+// in 0..n share one (a pad compares larger than every real key).  n <= W.
+template <int W>
+PCD_DEV bool order_exact(const GrpOrder<W>& o, int n, const LaneGrp<W>& g) {
+    const uint32_t k = o.s0;
+    const uint32_t aw = o.at(W);                      // (a shuffle: every lane of the group executes it)
+    const uint32_t dn = (uint32_t)__shfl_down((int)k, 1, W);
+    const uint32_t nxt = g.hl == W - 1 ? aw : dn;
+    const bool tie = g.hl < n && (k >> 8) == (nxt >> 8) && k != 0xFFFFFFFFu;
+    return !g.any(tie);
 }
 
-PCD_DEV unsigned long long wave_max_u64(unsigned long long v) {
+template <int W>
+PCD_DEV unsigned long long grp_max_u64(unsigned long long v) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long w = shfl_xor_u64(v, o);
+    for (int o = W / 2; o > 0; o >>= 1) {
+        const unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+        const unsigned long long w = (unsigned long long)(unsigned)__shfl_xor((int)lo, o, W) |
+                                     ((unsigned long long)(unsigned)__shfl_xor((int)hi, o, W) << 32);
         v = w > v ? w : v;
     }
     return v;
 }
 
 PCD_DEV uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-PCD_DEV unsigned long long rfl64(unsigned long long v) {
-    return (unsigned long long)rfl((uint32_t)v) | ((unsigned long long)rfl((uint32_t)(v >> 32)) << 32);
-}
 
-// Shrink a survivor set of more than 128 to at most 128 before ordering it (a 2-slot sort instead of 4): a few
-// bisection steps on d² find a bound with KA <= count(d² <= bound) <= 128; the keys under it contain the KA best
-// of the whole set (at least KA keys are under it), so the compaction never changes the result.
-template <int KA>
-PCD_DEV float rq_shrink(unsigned long long* buf, int& cnt, float capd2, int lane) {
+// Shrink a survivor set of more than 128 to at most 128 before ordering it: a few bisection steps on d² find a
+// bound with KA <= count(d² <= bound) <= 128; the keys under it contain the KA best of the whole set (at least KA
+// keys are under it), so the compaction never changes the result.
+template <int KA, int W>
+PCD_DEV float rq_shrink(unsigned long long* buf, int& cnt, float capd2, const LaneGrp<W>& g) {
+    constexpr int SL = RqSurv<W>::n / W;   // slots per lane
     if (cnt <= 128) return -1.f;
     wave_sync();
-    float d[4];
+    float d[SL];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const int e = s * 64 + lane;
+    for (int s = 0; s < SL; ++s) {
+        const int e = s * W + g.hl;
         d[s] = e < cnt ? __uint_as_float((uint32_t)(buf[e] >> 32)) : 3.0e38f;
     }
     auto count_le = [&](float t) {
         int c = 0;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) c += __popcll(__ballot(d[s] <= t));
+        for (int s = 0; s < SL; ++s) c += __popcll(g.ballot(d[s] <= t));
         return c;
     };
     float lo = 0.f, hi = capd2, bound = -1.f;
@@ -142,79 +179,85 @@ PCD_DEV float rq_shrink(unsigned long long* buf, int& cnt, float capd2, int lane
         else { bound = mid; break; }
     }
     if (bound < 0.f) return -1.f;                     // no such bound found quickly: order the full set
-    unsigned long long keep[4];
+    unsigned long long keep[SL];
     int base = 0;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) keep[s] = (s * 64 + lane) < cnt ? buf[s * 64 + lane] : 0ull;
+    for (int s = 0; s < SL; ++s) keep[s] = (s * W + g.hl) < cnt ? buf[s * W + g.hl] : 0ull;
     wave_sync();
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < SL; ++s) {
         const bool in = d[s] <= bound;
-        const unsigned long long m = __ballot(in);
-        if (in) buf[base + __popcll(m & ((1ull << lane) - 1ull))] = keep[s];
+        const unsigned long long m = g.ballot(in);
+        if (in) buf[base + __popcll(m & ((1ull << g.hl) - 1ull))] = keep[s];
         base += __popcll(m);
     }
     cnt = base;
     return bound;
 }
 
-// Cut the survivors to the K best (quantised order): false when the cut is ambiguous (the query must spill).
-template <int K>
-PCD_DEV bool rq_cut(unsigned long long* buf, int& cnt, unsigned long long& cap, int lane) {
+// Cut the survivors to the K best (quantised order; K <= 2W): false when the cut is ambiguous (the query spills).
+template <int K, int W>
+PCD_DEV bool rq_cut(unsigned long long* buf, int& cnt, unsigned long long& cap, const LaneGrp<W>& g) {
+    static_assert(K <= 2 * W, "the K best fit two slots of the group");
     {
-        const float bound = rq_shrink<K>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lane);
+        const float bound = rq_shrink<K, W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), g);
         if (bound >= 0.f) {                           // >= K keys have d² <= bound: a valid, tighter cap
             const unsigned long long c2 = ((unsigned long long)__float_as_uint(bound) << 32) | 0xFFFFFFFFull;
             if (c2 < cap) cap = c2;
             return true;
         }
     }
-    uint32_t after;
-    const uint32_t k = wave_order32(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lane, after);
-    const uint32_t kK = K < 64 ? (uint32_t)__shfl((int)k, K < 64 ? K : 0) : after;
-    const uint32_t kK1 = (uint32_t)__shfl((int)k, K - 1);
-    if ((kK >> 8) == (kK1 >> 8)) return false;
-    const unsigned long long mine = lane < K ? buf[k & 255u] : 0ull;
+    if (cnt > 4 * W) return false;                    // did not shrink (W = 32: more than 128 survivors)
+    const GrpOrder<W> o = grp_order32<W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), g);
+    if ((o.at(K) >> 8) == (o.at(K - 1) >> 8)) return false;
+    const bool h0 = g.hl < K, h1 = W + g.hl < K;
+    const unsigned long long m0 = h0 ? buf[o.s0 & 255u] : 0ull;
+    const unsigned long long m1 = h1 ? buf[o.s1 & 255u] : 0ull;
     wave_sync();
-    if (lane < K) buf[lane] = mine;
+    if (h0) buf[g.hl] = m0;
+    if (h1) buf[W + g.hl] = m1;
     wave_sync();
-    const unsigned long long mx = rfl64(wave_max_u64(lane < K ? mine : 0ull));
+    const unsigned long long mx = grp_max_u64<W>(m0 > m1 ? m0 : m1);
     if (mx + 1ull < cap) cap = mx + 1ull;
     cnt = K;
     return true;
 }
 
 // Scan the cells of box [lo, hi] (at most kRqMaxCells) appending keys < cap to buf: pcd_wknn.h wave_scan_box
-// in 32-bit cell arithmetic, with the quantised buffer cut.  Returns false when a cut was ambiguous (spill).
+// in 32-bit cell arithmetic, with the quantised buffer cut, for one lane group.  Returns false when a cut was
+// ambiguous (spill).
 static constexpr int kRqMaxCells = 4096;
 #ifndef PCD_RQ_ROWS
 #define PCD_RQ_ROWS 2
 #endif
 static constexpr int kRqRows = PCD_RQ_ROWS;   // candidate rows per lane per round (all loads in flight)
-#ifndef PCD_RQ_CPL
-#define PCD_RQ_CPL 1
+#ifndef PCD_RQ_CELLS
+#define PCD_RQ_CELLS 64
 #endif
-static constexpr int kRqCPL = PCD_RQ_CPL;     // cells per lane per chunk
-static constexpr int kRqChunk = 64 * kRqCPL;
-static constexpr int kRqChunkLog2 = kRqCPL == 1 ? 6 : kRqCPL == 2 ? 7 : 8;
-struct RqCells {            // per-wave LDS scratch for one chunk of cells
+static constexpr int kRqChunk = PCD_RQ_CELLS;  // cells per chunk (per group)
+template <int W> struct RqCPL { static constexpr int n = kRqChunk / W; };   // cells per lane per chunk
+static constexpr int kRqChunkLog2 = kRqChunk == 64 ? 6 : kRqChunk == 128 ? 7 : 8;
+struct RqCells {            // per-group LDS scratch for one chunk of cells
     uint32_t start[kRqChunk];
     uint32_t end_incl[kRqChunk];
 };
-template <int K>
+template <int K, int W>
 PCD_DEV bool rq_scan_box(const GridView& g, Vec3 q, const int lo[3], const int hi[3], unsigned long long& cap,
-                         unsigned long long* buf, int& cnt, RqCells* wc, int lane) {
-    static_assert(K + 64 * kRqRows <= kWaveSurv, "a cut to K plus one round of appends must fit the buffer");
+                         unsigned long long* buf, int& cnt, RqCells* wc, const LaneGrp<W>& lg) {
+    constexpr int CPL = RqCPL<W>::n;
+    static_assert(CPL >= 1 && CPL * W == kRqChunk, "chunk = whole cells per lane");
+    static_assert(K + W * kRqRows <= RqSurv<W>::n, "a cut to K plus one round of appends must fit the buffer");
+    const int hl = lg.hl;
     const int ex = hi[0] - lo[0] + 1, ey = hi[1] - lo[1] + 1;
     const int nc = ex * ey * (hi[2] - lo[2] + 1);
     const uint32_t exy = (uint32_t)ex * (uint32_t)ey;
     for (int base = 0; base < nc; base += kRqChunk) {
-        uint32_t slot[kRqCPL], loc6[kRqCPL];
-        unsigned long long bkey[kRqCPL];
+        uint32_t slot[CPL], loc6[CPL];
+        unsigned long long bkey[CPL];
         const float kth = __uint_as_float((unsigned)(cap >> 32));
 #pragma unroll
-        for (int u = 0; u < kRqCPL; ++u) {
-            const uint32_t ci = (uint32_t)(base + lane * kRqCPL + u);
+        for (int u = 0; u < CPL; ++u) {
+            const uint32_t ci = (uint32_t)(base + hl * CPL + u);
             slot[u] = ~0u; loc6[u] = 0; bkey[u] = kEmptyKey;
             if (ci < (uint32_t)nc) {
                 const uint32_t zq = ci / exy, rem = ci - zq * exy, yq = rem / (uint32_t)ex;
@@ -229,13 +272,13 @@ PCD_DEV bool rq_scan_box(const GridView& g, Vec3 q, const int lo[3], const int h
                 }
             }
         }
-        uint4 sl[kRqCPL];
+        uint4 sl[CPL];
 #pragma unroll
-        for (int u = 0; u < kRqCPL; ++u)
+        for (int u = 0; u < CPL; ++u)
             sl[u] = slot[u] != ~0u ? *reinterpret_cast<const uint4*>(g.table + slot[u]) : make_uint4(~0u, ~0u, 0u, 0u);
-        uint32_t brick[kRqCPL];
+        uint32_t brick[CPL];
 #pragma unroll
-        for (int u = 0; u < kRqCPL; ++u) {
+        for (int u = 0; u < CPL; ++u) {
             brick[u] = ~0u;
             if (slot[u] == ~0u) continue;
             uint4 e = sl[u];
@@ -248,39 +291,39 @@ PCD_DEV bool rq_scan_box(const GridView& g, Vec3 q, const int lo[3], const int h
                 e = *reinterpret_cast<const uint4*>(g.table + sidx);
             }
         }
-        uint2 cr[kRqCPL];
+        uint2 cr[CPL];
 #pragma unroll
-        for (int u = 0; u < kRqCPL; ++u)
+        for (int u = 0; u < CPL; ++u)
             cr[u] = brick[u] != ~0u ? g.cells[(uint64_t)brick[u] * 64 + loc6[u]] : make_uint2(0u, 0u);
-        uint32_t loc[kRqCPL], run = 0;
+        uint32_t loc[CPL], run = 0;
 #pragma unroll
-        for (int u = 0; u < kRqCPL; ++u) {
+        for (int u = 0; u < CPL; ++u) {
             run += cr[u].y > cr[u].x ? cr[u].y - cr[u].x : 0u;
             loc[u] = run;
         }
         uint32_t incl = run;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
-            if (lane >= o) incl += t;
+        for (int o = 1; o < W; o <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)incl, o, W);
+            if (hl >= o) incl += t;
         }
-        const uint32_t total = rfl((uint32_t)__shfl((int)incl, 63));
+        const uint32_t total = lg.bcast(incl, W - 1);
         if (total == 0) continue;
         const uint32_t excl = incl - run;
         wave_sync();
 #pragma unroll
-        for (int u = 0; u < kRqCPL; ++u) {
-            wc->start[lane * kRqCPL + u] = cr[u].x;
-            wc->end_incl[lane * kRqCPL + u] = excl + loc[u];
+        for (int u = 0; u < CPL; ++u) {
+            wc->start[hl * CPL + u] = cr[u].x;
+            wc->end_incl[hl * CPL + u] = excl + loc[u];
         }
         wave_sync();
-        for (uint32_t j0 = 0; j0 < total; j0 += 64 * kRqRows) {
+        for (uint32_t j0 = 0; j0 < total; j0 += W * kRqRows) {
             // room for a whole round of appends (one cut site: the sort network is inlined once)
-            if (cnt > kWaveSurv - 64 * kRqRows && !rq_cut<K>(buf, cnt, cap, lane)) return false;
+            if (cnt > RqSurv<W>::n - W * kRqRows && !rq_cut<K, W>(buf, cnt, cap, lg)) return false;
             uint32_t r[kRqRows];
 #pragma unroll
             for (int u = 0; u < kRqRows; ++u) {
-                const uint32_t j = j0 + (uint32_t)(u * 64 + lane);
+                const uint32_t j = j0 + (uint32_t)(u * W + hl);
                 int a = 0, b = kRqChunk - 1;
 #pragma unroll
                 for (int it = 0; it < kRqChunkLog2; ++it) {
@@ -292,18 +335,21 @@ PCD_DEV bool rq_scan_box(const GridView& g, Vec3 q, const int lo[3], const int h
             float px[kRqRows], py[kRqRows], pz[kRqRows];
 #pragma unroll
             for (int u = 0; u < kRqRows; ++u) {
-                if (j0 + (uint32_t)(u * 64) < total) {
+                if (j0 + (uint32_t)(u * W) < total) {
                     const float* pp = reinterpret_cast<const float*>(g.pts + r[u]);
                     px[u] = pp[0]; py[u] = pp[1]; pz[u] = pp[2];
                 }
             }
 #pragma unroll
             for (int u = 0; u < kRqRows; ++u) {
-                const uint32_t j = j0 + (uint32_t)(u * 64 + lane);
-                if (j0 + (uint32_t)(u * 64) < total) {
+                const uint32_t j = j0 + (uint32_t)(u * W + hl);
+                if (j0 + (uint32_t)(u * W) < total) {
                     const unsigned long long key2 =
                         ((unsigned long long)__float_as_uint(dist2(q, make_float4(px[u], py[u], pz[u], 0.f))) << 32) | r[u];
-                    wave_append(j < total && key2 < cap, key2, buf, cnt, lane);
+                    const bool pass = j < total && key2 < cap;
+                    const unsigned long long m = lg.ballot(pass);
+                    if (pass) buf[cnt + __popcll(m & ((1ull << hl) - 1ull))] = key2;
+                    cnt += __popcll(m);
                 }
             }
         }
@@ -322,9 +368,13 @@ struct RqStats { unsigned redo_cnt, spill_cnt, spill_big, spill_amb; };
 #ifndef PCD_RQ_OCC
 #define PCD_RQ_OCC 8
 #endif
-// One query per wave (grid-stride): DENSE = every active row (cap from the cell occupancy), else the rows of
-// `list` (the anchor test's failures, cap from the anchor).  Spilled rows go to `spill` for k_knn_redo_wave.
-template <int KA, bool DENSE>
+// One query per lane group of W lanes (grid-stride): DENSE = every active row (radius from the cell occupancy), else
+// the rows of `list` (the anchor test's failures, radius from the old anchor).  Spilled rows go to `spill` for
+// k_knn_redo_wave.
+#ifndef PCD_RQ_W
+#define PCD_RQ_W 64   // 32 (two queries per wave) measured equal at occupancy 6 and slower at 8 (spills)
+#endif
+template <int KA, bool DENSE, int W = PCD_RQ_W>
 __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, const float4* __restrict__ pos,
                                                                  int64_t N, RowMap rm, int kstore, float r_scale,
                                                                  float4* __restrict__ anc, int32_t* __restrict__ alist,
@@ -333,16 +383,20 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
                                                                  const unsigned* __restrict__ list_cnt,
                                                                  int32_t* __restrict__ spill,
                                                                  unsigned* __restrict__ spill_cnt) {
-    static_assert(KA <= 64, "one key per lane");
-    __shared__ unsigned long long s_buf[4][kWaveSurv];
-    __shared__ RqCells s_cells[4];
+    static_assert(KA <= 2 * W && KA <= 64, "the anchor set fits two slots of the group");
+    constexpr int G = 64 / W;                    // groups (queries in flight) per wave
+    __shared__ unsigned long long s_buf[4 * G][RqSurv<W>::n];
+    __shared__ RqCells s_cells[4 * G];
     const int lane = (int)(threadIdx.x & 63);
+    const LaneGrp<W> lg(lane);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int gid = wv * G + lane / W;           // group in the block
     const int64_t cnt_rows = DENSE ? rm.nq : (int64_t)*list_cnt;
     const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
-    unsigned long long* buf = s_buf[wv];
-    for (int64_t t0 = lb * 4 + wv; t0 < cnt_rows; t0 += (int64_t)gridDim.x * 4) {
-        const int64_t i = __builtin_amdgcn_readfirstlane(DENSE ? (int)rm(t0) : list[t0]);
+    unsigned long long* buf = s_buf[gid];
+    for (int64_t t0 = lb * 4 * G + gid; t0 < cnt_rows; t0 += (int64_t)gridDim.x * 4 * G) {
+        int64_t i = DENSE ? rm(t0) : (int64_t)list[t0];
+        if (W == 64) i = (int64_t)rfl((uint32_t)i);
         const float4 p4 = pos[i];
         const Vec3 q = v3(p4.x, p4.y, p4.z);
         // The search radius r: DENSE from the occupancy of the query's cell, else from the old anchor's D (the local
@@ -360,7 +414,7 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
         } else {
             const float4 a = anc[i];
             if (!(a.w > 0.f)) {                       // no anchor: the wave search grows its own box
-                if (lane == 0) spill[atomicAdd(spill_cnt, 1u)] = (int32_t)i;
+                if (lg.hl == 0) spill[atomicAdd(spill_cnt, 1u)] = (int32_t)i;
                 continue;
             }
             r_s = a.w * PCD_RQ_RSCALE;
@@ -380,48 +434,48 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
             const int64_t nbox = (int64_t)(hi[0] - lo[0] + 1) * (hi[1] - lo[1] + 1) * (hi[2] - lo[2] + 1);
             big = nbox > kRqMaxCells;
             if (big) break;
-            const bool clean = rq_scan_box<KA>(g, q, lo, hi, cap, buf, cnt, &s_cells[wv], lane);
+            const bool clean = rq_scan_box<KA, W>(g, q, lo, hi, cap, buf, cnt, &s_cells[gid], lg);
             ok = clean && cnt > kstore;
             if (ok || !clean) break;
             wave_sync();
         }
         const bool partial = cnt < KA;               // (after a buffer cut cnt == KA)
-        uint32_t k = 0xFFFFFFFFu;
+        GrpOrder<W> o{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, &lg};
         if (ok) {
-            uint32_t after;
-            (void)rq_shrink<KA>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lane);
-            k = wave_order32(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lane, after);
+            (void)rq_shrink<KA, W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lg);
+            ok = cnt <= 4 * W;                        // (a set that did not shrink to 4W spills)
+        }
+        if (ok) {
+            o = grp_order32<W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lg);
             // exact order of the stored list (first kstore + its successor) and of the anchor set boundary
-            ok = order_exact(k, after, kstore, lane);
-            const uint32_t kK = KA < 64 ? (uint32_t)__shfl((int)k, KA < 64 ? KA : 0) : after;  // element KA
-            const uint32_t kK1 = (uint32_t)__shfl((int)k, KA - 1);
-            ok = ok && (cnt <= KA || (kK >> 8) != (kK1 >> 8));
+            ok = order_exact<W>(o, kstore, lg);
+            ok = ok && (cnt <= KA || (o.at(KA) >> 8) != (o.at(KA - 1) >> 8));
         }
         if (!ok) {
             wave_sync();
-            if (lane == 0) {
+            if (lg.hl == 0) {
                 spill[atomicAdd(spill_cnt, 1u)] = (int32_t)i;
                 atomicAdd(big ? spill_cnt + 1 : spill_cnt + 2, 1u);   // RqStats::spill_big / spill_amb
             }
             continue;
         }
-        const bool have = lane < KA && lane < cnt;
-        const unsigned long long mine = have ? buf[k & 255u] : 0ull;
-        // unused slots of a partial set hold -1 (the anchor test gives them an infinite distance)
-        const int32_t r = have ? (int32_t)(uint32_t)(mine & 0xFFFFFFFFull) : -1;
-#if defined(PCD_EXP_RQ_WRITE) && PCD_EXP_RQ_WRITE == 1      // timing experiment: no list writes (results wrong)
-        if (r == -12345) alist[i] = r;
-#elif defined(PCD_EXP_RQ_WRITE) && PCD_EXP_RQ_WRITE == 2    // timing experiment: contiguous writes (results wrong)
-        if (lane < KA) alist[t0 * 64 + lane] = r;
-#else
-        if (lane < KA) alist[(int64_t)lane * N + i] = r;
-        if (lane < kstore) idx[(int64_t)lane * N + i] = r;
-#endif
+        // this lane's elements hl and W + hl of the order; unused slots of a partial set hold -1 (the anchor test
+        // gives them an infinite distance)
+        const int e0 = lg.hl, e1 = W + lg.hl;
+        const bool h0 = e0 < KA && e0 < cnt, h1 = e1 < KA && e1 < cnt;
+        const unsigned long long m0 = h0 ? buf[o.s0 & 255u] : 0ull;
+        const unsigned long long m1 = h1 ? buf[o.s1 & 255u] : 0ull;
+        const int32_t r0 = h0 ? (int32_t)(uint32_t)(m0 & 0xFFFFFFFFull) : -1;
+        const int32_t r1 = h1 ? (int32_t)(uint32_t)(m1 & 0xFFFFFFFFull) : -1;
+        if (e0 < KA) alist[(int64_t)e0 * N + i] = r0;
+        if (e1 < KA) alist[(int64_t)e1 * N + i] = r1;
+        if (e0 < kstore) idx[(int64_t)e0 * N + i] = r0;
+        if (e1 < kstore) idx[(int64_t)e1 * N + i] = r1;
         // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
         // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))
-        const unsigned long long mx = wave_max_u64(mine);
+        const unsigned long long mx = grp_max_u64<W>(m0 > m1 ? m0 : m1);
         const float D = partial ? r_s * (1.f - 1e-6f) : sqrtf(__uint_as_float((unsigned)(mx >> 32)));
-        if (lane == 0) anc[i] = make_float4(q.x, q.y, q.z, D);
+        if (lg.hl == 0) anc[i] = make_float4(q.x, q.y, q.z, D);
         wave_sync();                                  // buf is free for the next query
     }
 }
