@@ -408,8 +408,12 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
         const int32_t r = valid ? (int32_t)r32 : (int32_t)i;
         const bool all_valid = !__any(lane < KA && !valid);
         if (!all_valid && lane == 0) atomicOr(err, 1);
-        if (lane < KA) alist[(int64_t)lane * N + i] = r;
         if (lane < kstore) idx[(int64_t)lane * N + i] = r;
+        {   // the anchor set in rank order (see k_knn_requery), unused slots last
+            uint32_t v[1] = {lane < KA ? (uint32_t)r : 0xFFFFFFFFu};
+            grp_bitonic_sort32<64, 1>(v, lane);
+            if (lane < KA) alist[(int64_t)lane * N + i] = (int32_t)v[0];
+        }
         // D: the KA-th distance (every other snapshot point is at least this far from the anchor)
         if (lane == KA - 1)
             anc[i] = make_float4(q.x, q.y, q.z, all_valid ? sqrtf(__uint_as_float((unsigned)(top >> 32))) : __int_as_float(0x7FC00000));

@@ -467,10 +467,20 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
         const unsigned long long m1 = h1 ? buf[o.s1 & 255u] : 0ull;
         const int32_t r0 = h0 ? (int32_t)(uint32_t)(m0 & 0xFFFFFFFFull) : -1;
         const int32_t r1 = h1 ? (int32_t)(uint32_t)(m1 & 0xFFFFFFFFull) : -1;
-        if (e0 < KA) alist[(int64_t)e0 * N + i] = r0;
-        if (e1 < KA) alist[(int64_t)e1 * N + i] = r1;
         if (e0 < kstore) idx[(int64_t)e0 * N + i] = r0;
         if (e1 < kstore) idx[(int64_t)e1 * N + i] = r1;
+        // the anchor set is stored in RANK order (unused slots last): the anchor test ranks it by distance itself,
+        // and neighbouring rows -- neighbouring lanes of its waves -- then gather nearly the same snapshot rows in the
+        // same slot, i.e. the same cache lines, instead of 64 unrelated ones per gather instruction
+        {
+            constexpr int M = KA > W ? 2 : 1;
+            uint32_t v[M];
+            v[0] = e0 < KA ? (uint32_t)r0 : 0xFFFFFFFFu;
+            if (M > 1) v[M - 1] = e1 < KA ? (uint32_t)r1 : 0xFFFFFFFFu;
+            grp_bitonic_sort32<W, M>(v, lg.hl);
+            if (e0 < KA) alist[(int64_t)e0 * N + i] = (int32_t)v[0];
+            if (M > 1 && e1 < KA) alist[(int64_t)e1 * N + i] = (int32_t)v[M - 1];
+        }
         // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
         // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))
         const unsigned long long mx = grp_max_u64<W>(m0 > m1 ? m0 : m1);

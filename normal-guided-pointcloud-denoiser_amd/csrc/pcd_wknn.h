@@ -129,15 +129,167 @@ PCD_DEV void wave_append(bool pass, unsigned long long key, unsigned long long* 
     cnt += __popcll(m);
 }
 
+// Steps 3+ of a chunk: this lane's kCellsPerLane cell row ranges cr -> flattened candidate rows -> keys < cap
+// appended to buf (a full buffer is cut to the K best and the cap tightened).
+#ifndef PCD_WAVE_ROWS
+#define PCD_WAVE_ROWS 4
+#endif
+static constexpr int kWaveRows = PCD_WAVE_ROWS;
+template <int K>
+PCD_DEV void wave_scan_chunk(const GridView& g, Vec3 q, const uint2 (&cr)[kCellsPerLane], unsigned long long& cap,
+                             unsigned long long* buf, int& cnt, WaveCells* wc, int lane) {
+    uint32_t loc[kCellsPerLane], run = 0;
+#pragma unroll
+    for (int u = 0; u < kCellsPerLane; ++u) {
+        run += cr[u].y > cr[u].x ? cr[u].y - cr[u].x : 0u;
+        loc[u] = run;
+    }
+    uint32_t incl = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
+        if (lane >= o) incl += t;
+    }
+    const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+    PCD_WSTAT(1, 1);
+    PCD_WSTAT(2, total);
+    if (total == 0) return;
+    const uint32_t excl = incl - run;
+    wave_sync();                         // the previous chunk's readers are done with wc
+#pragma unroll
+    for (int u = 0; u < kCellsPerLane; ++u) {
+        wc->start[lane * kCellsPerLane + u] = cr[u].x;
+        wc->end_incl[lane * kCellsPerLane + u] = excl + loc[u];
+    }
+    wave_sync();
+    for (uint32_t j0 = 0; j0 < total; j0 += 64 * kWaveRows) {
+        uint32_t r[kWaveRows];
+#pragma unroll
+        for (int u = 0; u < kWaveRows; ++u) {
+            const uint32_t j = j0 + (uint32_t)(u * 64 + lane);
+            r[u] = 0u;
+            if (j0 + (uint32_t)(u * 64) >= total) continue;   // wave-uniform: slot past the chunk
+            int a = 0, b = kChunkCells - 1;   // first cell whose inclusive end exceeds j
+#pragma unroll
+            for (int it = 0; it < kChunkLog2; ++it) {
+                const int m = (a + b) >> 1;
+                if (wc->end_incl[m] > j) b = m; else a = m + 1;
+            }
+            r[u] = j < total ? wc->start[a] + (j - (a ? wc->end_incl[a - 1] : 0u)) : 0u;
+        }
+        float4 p[kWaveRows];
+#pragma unroll
+        for (int u = 0; u < kWaveRows; ++u)
+            if (j0 + (uint32_t)(u * 64) < total) p[u] = g.pts[r[u]];
+#pragma unroll
+        for (int u = 0; u < kWaveRows; ++u) {
+            const uint32_t j = j0 + (uint32_t)(u * 64 + lane);
+            if (j0 + (uint32_t)(u * 64) < total) {
+                if (cnt > kWaveSurv - 64) {  // make room: keep the K best, tighten the cap
+                    PCD_WSTAT(3, 1);
+                    int kept;
+                    const unsigned long long top = wave_sort_survivors(buf, cnt, lane, K, kept);
+                    const unsigned long long kth_key = __shfl(top, K - 1);
+                    if (kept == K && kth_key + 1ull < cap) cap = kth_key + 1ull;
+                    cnt = kept;
+                }
+                const unsigned long long key2 = cand_key<false>(q, p[u], r[u]);
+                wave_append(j < total && key2 < cap, key2, buf, cnt, lane);
+            }
+        }
+        wave_sync();
+    }
+}
+
+PCD_DEV bool cell_near(const GridView& g, Vec3 q, int cx, int cy, int cz, float kth) {
+    const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
+    const float gx = axis_gap(q.x, lx, lx + g.h), gy = axis_gap(q.y, ly, ly + g.h), gz = axis_gap(q.z, lz, lz + g.h);
+    return gx * gx + gy * gy + gz * gz <= kth * 1.00001f + 1e-30f;
+}
+
+// Boxes of more than kBrickModeCells cells (far outliers, sparse regions, the growing blocks of an anchorless query)
+// are walked brick by brick: one lane probes one 4x4x4 brick (one hash lookup for 64 cells, pruned by its box
+// distance), the occupied bricks are compacted in LDS, and each then yields its 64 cell ranges from its dense block
+// with no further probes -- empty space costs one probe per 64 cells instead of one per cell.
+static constexpr int64_t kBrickModeCells = 1024;
+PCD_DEV void cell_of_brick(int l, int& dx, int& dy, int& dz) {   // Morton decode of the low 6 key bits
+    dx = (l & 1) | ((l >> 2) & 2);
+    dy = ((l >> 1) & 1) | ((l >> 3) & 2);
+    dz = ((l >> 2) & 1) | ((l >> 4) & 2);
+}
+template <int K>
+PCD_DEV void wave_scan_bricks(const GridView& g, Vec3 q, const int lo[3], const int hi[3], unsigned long long& cap,
+                              unsigned long long* buf, int& cnt, WaveCells* wc, int lane) {
+    static_assert(kCellsPerLane == 2, "two bricks per chunk: lane l takes cell l of each");
+    const int blo[3] = {lo[0] >> 2, lo[1] >> 2, lo[2] >> 2}, bhi[3] = {hi[0] >> 2, hi[1] >> 2, hi[2] >> 2};
+    const int ex = bhi[0] - blo[0] + 1, ey = bhi[1] - blo[1] + 1, ez = bhi[2] - blo[2] + 1;
+    const int64_t nb = (int64_t)ex * ey * ez;
+    // the found bricks of a probe round go to wc (brick id, bx, by, bz in four 64-entry quarters), then into
+    // registers (wave_scan_chunk reuses wc)
+    for (int64_t base = 0; base < nb; base += 64) {
+        const int64_t bi = base + lane;
+        uint32_t brick = ~0u;
+        int bx = 0, by = 0, bz = 0;
+        if (bi < nb) {
+            bx = blo[0] + (int)(bi % ex); by = blo[1] + (int)((bi / ex) % ey); bz = blo[2] + (int)(bi / ((int64_t)ex * ey));
+            // brick box distance
+            const float lx = g.ox + (bx * 4) * g.h, ly = g.oy + (by * 4) * g.h, lz = g.oz + (bz * 4) * g.h;
+            const float w = 4.f * g.h;
+            const float gx = axis_gap(q.x, lx, lx + w), gy = axis_gap(q.y, ly, ly + w), gz = axis_gap(q.z, lz, lz + w);
+            const float kth = __uint_as_float((unsigned)(cap >> 32));
+            if (gx * gx + gy * gy + gz * gz <= kth * 1.00001f + 1e-30f) {
+                const unsigned long long bkey = morton3(bx, by, bz);
+                unsigned long long slot = hash_slot(bkey, g.hbits);
+                for (;;) {
+                    const uint4 e = *reinterpret_cast<const uint4*>(g.table + slot);
+                    const unsigned long long k2 = (unsigned long long)e.x | ((unsigned long long)e.y << 32);
+                    if (k2 == bkey) { brick = e.z; break; }
+                    if (k2 == kEmptyKey) break;
+                    slot = (slot + 1) & g.mask;
+                }
+            }
+        }
+        const unsigned long long found = __ballot(brick != ~0u);
+        const int nf = __popcll(found);
+        if (nf == 0) continue;
+        // this lane's found brick -> position in the compacted list (registers: bid / packed coords by shuffle)
+        const int pos = __popcll(found & ((1ull << lane) - 1ull));
+        wave_sync();
+        if (brick != ~0u) {
+            wc->start[pos] = brick;
+            wc->start[64 + pos] = (uint32_t)bx;
+            wc->end_incl[pos] = (uint32_t)by;
+            wc->end_incl[64 + pos] = (uint32_t)bz;
+        }
+        wave_sync();
+        const uint32_t my_b = lane < nf ? wc->start[lane] : 0u, my_x = lane < nf ? wc->start[64 + lane] : 0u,
+                       my_y = lane < nf ? wc->end_incl[lane] : 0u, my_z = lane < nf ? wc->end_incl[64 + lane] : 0u;
+        wave_sync();
+        for (int f = 0; f < nf; f += 2) {            // two bricks per chunk
+            uint2 cr[kCellsPerLane];
+            const float kth = __uint_as_float((unsigned)(cap >> 32));
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                cr[u] = make_uint2(0u, 0u);
+                if (f + u >= nf) continue;          // wave-uniform
+                const uint32_t b = (uint32_t)__shfl((int)my_b, f + u);
+                int dx, dy, dz;
+                cell_of_brick(lane, dx, dy, dz);
+                const int cx = __shfl((int)my_x, f + u) * 4 + dx, cy = __shfl((int)my_y, f + u) * 4 + dy,
+                          cz = __shfl((int)my_z, f + u) * 4 + dz;
+                const bool inbox = cx >= lo[0] && cx <= hi[0] && cy >= lo[1] && cy <= hi[1] && cz >= lo[2] && cz <= hi[2];
+                if (inbox && cell_near(g, q, cx, cy, cz, kth)) cr[u] = g.cells[(uint64_t)b * 64 + lane];
+            }
+            wave_scan_chunk<K>(g, q, cr, cap, buf, cnt, wc, lane);
+        }
+    }
+}
+
 // Scan the cells of box [lo, hi] (cell coords), appending keys < cap to buf.  cap may tighten (buffer reduce).
 // Latency-shaped: a chunk is up to 256 cells (the whole cap box of a typical query), kCellsPerLane per lane, whose
 // brick-hash probes, then brick-block loads, are each issued together (two memory round trips for the chunk);
 // then the chunk's flattened candidate rows in rounds of kWaveRows per lane -- every row index first (binary search
 // of the count scan in LDS), then all the point loads at once, then the keys.
-#ifndef PCD_WAVE_ROWS
-#define PCD_WAVE_ROWS 4
-#endif
-static constexpr int kWaveRows = PCD_WAVE_ROWS;
 template <int K>
 PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int hi[3], unsigned long long& cap,
                            unsigned long long* buf, int& cnt, WaveCells* wc, int lane) {
@@ -145,7 +297,10 @@ PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int
     // whose box is clamped to the grid; 64-bit only for the (rare) giant product
     const int ex = hi[0] - lo[0] + 1, ey = hi[1] - lo[1] + 1, ez = hi[2] - lo[2] + 1;
     const int64_t nc = (int64_t)ex * ey * ez;
-    const bool small = nc < (1ll << 31);
+    if (nc > kBrickModeCells) {
+        wave_scan_bricks<K>(g, q, lo, hi, cap, buf, cnt, wc, lane);
+        return;
+    }
     const uint32_t exy = (uint32_t)ex * (uint32_t)ey;
     for (int64_t base = 0; base < nc; base += kChunkCells) {
         // 1. this lane's cells (lane-major: cells lane*CPL .. +CPL-1 of the chunk): prune, hash slot, probe
@@ -159,16 +314,9 @@ PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int
             want[u] = false;
             key[u] = 0; slot[u] = 0;
             if (ci < nc) {
-                int cx, cy, cz;
-                if (small) {
-                    const uint32_t c32 = (uint32_t)ci, zq = c32 / exy, rem = c32 - zq * exy, yq = rem / (uint32_t)ex;
-                    cx = lo[0] + (int)(rem - yq * (uint32_t)ex); cy = lo[1] + (int)yq; cz = lo[2] + (int)zq;
-                } else {
-                    cx = lo[0] + (int)(ci % ex); cy = lo[1] + (int)((ci / ex) % ey); cz = lo[2] + (int)(ci / ((int64_t)ex * ey));
-                }
-                const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
-                const float gx = axis_gap(q.x, lx, lx + g.h), gy = axis_gap(q.y, ly, ly + g.h), gz = axis_gap(q.z, lz, lz + g.h);
-                if (gx * gx + gy * gy + gz * gz <= kth * 1.00001f + 1e-30f) {
+                const uint32_t c32 = (uint32_t)ci, zq = c32 / exy, rem = c32 - zq * exy, yq = rem / (uint32_t)ex;
+                const int cx = lo[0] + (int)(rem - yq * (uint32_t)ex), cy = lo[1] + (int)yq, cz = lo[2] + (int)zq;
+                if (cell_near(g, q, cx, cy, cz, kth)) {
                     want[u] = true;
                     key[u] = morton3(cx, cy, cz);
                     slot[u] = hash_slot(key[u] >> 6, g.hbits);
@@ -199,68 +347,7 @@ PCD_DEV void wave_scan_box(const GridView& g, Vec3 q, const int lo[3], const int
 #pragma unroll
         for (int u = 0; u < kCellsPerLane; ++u)
             cr[u] = brick[u] != ~0u ? g.cells[(uint64_t)brick[u] * 64 + (key[u] & 63)] : make_uint2(0u, 0u);
-        // 3. counts -> lane-local prefix -> wave exclusive scan of the lane totals
-        uint32_t loc[kCellsPerLane], run = 0;
-#pragma unroll
-        for (int u = 0; u < kCellsPerLane; ++u) {
-            run += cr[u].y > cr[u].x ? cr[u].y - cr[u].x : 0u;
-            loc[u] = run;
-        }
-        uint32_t incl = run;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
-            if (lane >= o) incl += t;
-        }
-        const uint32_t total = (uint32_t)__shfl((int)incl, 63);
-        PCD_WSTAT(1, 1);
-        PCD_WSTAT(2, total);
-        if (total == 0) continue;
-        const uint32_t excl = incl - run;
-        wave_sync();                         // the previous chunk's readers are done with wc
-#pragma unroll
-        for (int u = 0; u < kCellsPerLane; ++u) {
-            wc->start[lane * kCellsPerLane + u] = cr[u].x;
-            wc->end_incl[lane * kCellsPerLane + u] = excl + loc[u];
-        }
-        wave_sync();
-        for (uint32_t j0 = 0; j0 < total; j0 += 64 * kWaveRows) {
-            uint32_t r[kWaveRows];
-#pragma unroll
-            for (int u = 0; u < kWaveRows; ++u) {
-                const uint32_t j = j0 + (uint32_t)(u * 64 + lane);
-                r[u] = 0u;
-                if (j0 + (uint32_t)(u * 64) >= total) continue;   // wave-uniform: slot past the chunk
-                int a = 0, b = kChunkCells - 1;   // first cell whose inclusive end exceeds j
-#pragma unroll
-                for (int it = 0; it < kChunkLog2; ++it) {
-                    const int m = (a + b) >> 1;
-                    if (wc->end_incl[m] > j) b = m; else a = m + 1;
-                }
-                r[u] = j < total ? wc->start[a] + (j - (a ? wc->end_incl[a - 1] : 0u)) : 0u;
-            }
-            float4 p[kWaveRows];
-#pragma unroll
-            for (int u = 0; u < kWaveRows; ++u)
-                if (j0 + (uint32_t)(u * 64) < total) p[u] = g.pts[r[u]];
-#pragma unroll
-            for (int u = 0; u < kWaveRows; ++u) {
-                const uint32_t j = j0 + (uint32_t)(u * 64 + lane);
-                if (j0 + (uint32_t)(u * 64) < total) {
-                    if (cnt > kWaveSurv - 64) {  // make room: keep the K best, tighten the cap
-                        PCD_WSTAT(3, 1);
-                        int kept;
-                        const unsigned long long top = wave_sort_survivors(buf, cnt, lane, K, kept);
-                        const unsigned long long kth_key = __shfl(top, K - 1);
-                        if (kept == K && kth_key + 1ull < cap) cap = kth_key + 1ull;
-                        cnt = kept;
-                    }
-                    const unsigned long long key2 = cand_key<false>(q, p[u], r[u]);
-                    wave_append(j < total && key2 < cap, key2, buf, cnt, lane);
-                }
-            }
-            wave_sync();
-        }
+        wave_scan_chunk<K>(g, q, cr, cap, buf, cnt, wc, lane);
     }
 }
 
