@@ -73,7 +73,7 @@ PCD_DEV void grp_bitonic_sort32(uint32_t (&v)[M], int hl) {
 #pragma unroll
                 for (int s = 0; s < M; ++s) {
                     const bool asc = ((s * W + hl) & size) == 0;
-                    const uint32_t o = (uint32_t)__shfl_xor((int)v[s], stride, W);
+                    const uint32_t o = lane_xor(v[s], stride);   // stride < W: stays inside the group
                     v[s] = (lower == asc) ? min(o, v[s]) : max(o, v[s]);
                 }
             }
@@ -140,8 +140,7 @@ PCD_DEV unsigned long long grp_max_u64(unsigned long long v) {
 #pragma unroll
     for (int o = W / 2; o > 0; o >>= 1) {
         const unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
-        const unsigned long long w = (unsigned long long)(unsigned)__shfl_xor((int)lo, o, W) |
-                                     ((unsigned long long)(unsigned)__shfl_xor((int)hi, o, W) << 32);
+        const unsigned long long w = (unsigned long long)lane_xor(lo, o) | ((unsigned long long)lane_xor(hi, o) << 32);
         v = w > v ? w : v;
     }
     return v;
@@ -301,12 +300,7 @@ PCD_DEV bool rq_scan_box(const GridView& g, Vec3 q, const int lo[3], const int h
             run += cr[u].y > cr[u].x ? cr[u].y - cr[u].x : 0u;
             loc[u] = run;
         }
-        uint32_t incl = run;
-#pragma unroll
-        for (int o = 1; o < W; o <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)incl, o, W);
-            if (hl >= o) incl += t;
-        }
+        const uint32_t incl = lane_scan_incl<W>(run);
         const uint32_t total = lg.bcast(incl, W - 1);
         if (total == 0) continue;
         const uint32_t excl = incl - run;
@@ -317,6 +311,9 @@ PCD_DEV bool rq_scan_box(const GridView& g, Vec3 q, const int lo[3], const int h
             wc->end_incl[hl * CPL + u] = excl + loc[u];
         }
         wave_sync();
+#if defined(PCD_EXP_RQ) && PCD_EXP_RQ == 2    // timing experiment: cell phase only (results wrong)
+        if (total != 0x7FFFFFFF) { wave_sync(); continue; }
+#endif
         for (uint32_t j0 = 0; j0 < total; j0 += W * kRqRows) {
             // room for a whole round of appends (one cut site: the sort network is inlined once)
             if (cnt > RqSurv<W>::n - W * kRqRows && !rq_cut<K, W>(buf, cnt, cap, lg)) return false;
@@ -439,6 +436,9 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
             if (ok || !clean) break;
             wave_sync();
         }
+#if defined(PCD_EXP_RQ) && PCD_EXP_RQ >= 1    // timing experiment: no ordering / writes (results wrong)
+        if (cnt != -7) { wave_sync(); continue; }
+#endif
         const bool partial = cnt < KA;               // (after a buffer cut cnt == KA)
         GrpOrder<W> o{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, &lg};
         if (ok) {

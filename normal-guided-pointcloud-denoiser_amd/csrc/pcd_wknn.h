@@ -33,10 +33,46 @@ PCD_DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Cross-lane exchange with lane ^ s for a constant s (the unrolled sort / reduction networks): DPP moves for s <= 8
+// (quad_perm, row half-mirror / mirror compositions) and the CDNA4 permlane16/32 swaps for 16 / 32 -- VALU-native,
+// where __shfl_xor compiles to ds_bpermute (an LDS-crossbar round trip on every stage of a dependent network).
+//   s = 4: quad_perm[3,2,1,0] (l^3) then row_half_mirror (l^7) -> l^4;   s = 8: half_mirror (l^7) then row_mirror (l^15)
+PCD_DEV uint32_t lane_xor(uint32_t v, int s) {
+    switch (s) {
+        case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+        case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+        case 4: {
+            const int t = __builtin_amdgcn_mov_dpp((int)v, 0x1B, 0xF, 0xF, false);
+            return (uint32_t)__builtin_amdgcn_mov_dpp(t, 0x141, 0xF, 0xF, false);
+        }
+        case 8: {
+            const int t = __builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+            return (uint32_t)__builtin_amdgcn_mov_dpp(t, 0x140, 0xF, 0xF, false);
+        }
+        case 16: {   // swap odd rows of the first operand with even rows of the second
+            const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+            return (__lane_id() & 16) ? p[0] : p[1];
+        }
+        case 32: {   // swap the upper half of the first operand with the lower half of the second
+            const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            return (__lane_id() & 32) ? p[0] : p[1];
+        }
+        default: return (uint32_t)__shfl_xor((int)v, s);
+    }
+}
 PCD_DEV unsigned long long shfl_xor_u64(unsigned long long v, int m) {
-    const unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
-    return (unsigned long long)(unsigned)__shfl_xor((int)lo, m) |
-           ((unsigned long long)(unsigned)__shfl_xor((int)hi, m) << 32);
+    return (unsigned long long)lane_xor((uint32_t)v, m) | ((unsigned long long)lane_xor((uint32_t)(v >> 32), m) << 32);
+}
+// Inclusive prefix sum over groups of W = 32 or 64 lanes (DPP row shifts inside rows of 16, then the row broadcasts).
+template <int W>
+PCD_DEV uint32_t lane_scan_incl(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    if (W == 64) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return x;
 }
 
 // Ascending bitonic sort of the 64*M keys v[s] (element e = s*64 + lane) across the wave.
@@ -144,12 +180,7 @@ PCD_DEV void wave_scan_chunk(const GridView& g, Vec3 q, const uint2 (&cr)[kCells
         run += cr[u].y > cr[u].x ? cr[u].y - cr[u].x : 0u;
         loc[u] = run;
     }
-    uint32_t incl = run;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
-        if (lane >= o) incl += t;
-    }
+    const uint32_t incl = lane_scan_incl<64>(run);
     const uint32_t total = (uint32_t)__shfl((int)incl, 63);
     PCD_WSTAT(1, 1);
     PCD_WSTAT(2, total);
