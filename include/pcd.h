@@ -232,7 +232,8 @@ int pcd_denoiser_set_coverage(pcd_denoiser* dn, const float* lo3, const float* h
  * float[1] delta, nullable = local value). */
 int pcd_denoiser_stage(pcd_denoiser* dn, const pcd_denoise_params* p, int stage, int phase, void* red,
                        void* stream);
-/* state rows <-> packed device float4 buffers (field PCD_FIELD_*; POS = current positions). */
+/* state rows <-> packed device float4 buffers (field PCD_FIELD_*; POS = current positions).  FN rows unpacked
+ * between K1 and NVT2 must be another rank's K1 output (unit vectors: NVT2's vote margin assumes it). */
 int pcd_denoiser_pack(pcd_denoiser* dn, int field, const int32_t* rows, int64_t n, float* out4, void* stream);
 int pcd_denoiser_unpack(pcd_denoiser* dn, int field, const int32_t* rows, int64_t n, const float* in4,
                         void* stream);

@@ -65,6 +65,9 @@ static constexpr int kWinHaloNvt2 = 512;
 static constexpr int kWinHaloPhase = 128;
 template <int H> struct WinSize { static constexpr int rows = 256 + 2 * H; };
 static constexpr int kWinRows = WinSize<kWinHalo>::rows;
+#ifndef PCD_WIN_SPLIT
+#define PCD_WIN_SPLIT 0
+#endif
 template <int H = kWinHalo>
 struct WinRows {
     const float4* g;
@@ -73,8 +76,17 @@ struct WinRows {
     PCD_DEV Vec3 operator()(int64_t j) const {
         const uint64_t o = (uint64_t)(j - lo);
         float4 q;
+#if PCD_WIN_SPLIT
+        // every lane reads LDS (a clamped slot), only the lanes outside the window issue a global load: the two
+        // loads cannot be merged into one flat load, which would send every lane through the texture path
+        const bool in = o < (uint64_t)WinSize<H>::rows;
+        const float4 sv = s[in ? o : 0];
+        if (in) q = sv;
+        else q = g[j];
+#else
         if (o < (uint64_t)WinSize<H>::rows) q = s[o];
         else q = g[j];
+#endif
         return v3(q.x, q.y, q.z);
     }
 };
@@ -307,7 +319,7 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
 
 // NVT1 + eigh + VU smoothing over the stored lists (lane per row); checks every list entry and, for spatial slabs,
 // that the kstore-ball stays inside the local snapshot.
-template <int K, class P, class Nr>
+template <int K, bool UNIT, class P, class Nr>
 __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
                       const int32_t* __restrict__ idx, int64_t N, int64_t i, int k, int kstore, float rho, float tau,
                       float damp, const Cover& cov, float4* __restrict__ fn, int* __restrict__ err, P rp, Nr rn) {
@@ -328,7 +340,7 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
             if (t == kstore - 1) dk = dist2(vi, g.pts[l[t]]);
         if (!cov.holds(vi, dk)) atomicOr(err, 2);
     }
-    const Sym3 T = nvt_tensor<K>(rp, rn, vi, k, RegNb32{l}, rho, ColNbSafe{idx, N, i});
+    const Sym3 T = nvt_tensor<K, true, UNIT>(rp, rn, vi, k, RegNb32{l}, rho, ColNbSafe{idx, N, i});
     float w[3], V[3][3];
     eigh3(T, w, V);
     const float4 n4 = nrm[i];
@@ -338,7 +350,9 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
 
 // Every active row, or (skip != null) every active row t with skip[t] == 0: the rows the anchor test certified,
 // run on a side stream while the re-anchoring search works on the others (pcd_denoiser::side).
-template <int K>
+// UNIT: the normals are the loop's own normalised f_n (every iteration after the first since load): the vote's
+// margin is a constant (nvt_tensor).
+template <int K, bool UNIT>
 __global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                int kstore, float rho, float tau, float damp, Cover cov,
@@ -350,7 +364,7 @@ __global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restri
     const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
     if (skip && skip[t0]) return;
-    nvt1_row<K>(g, pos, nrm, idx, N, rm(t0), k, kstore, rho, tau, damp, cov, fn, err, WinRows<>{pos, s_pos, lo},
+    nvt1_row<K, UNIT>(g, pos, nrm, idx, N, rm(t0), k, kstore, rho, tau, damp, cov, fn, err, WinRows<>{pos, s_pos, lo},
                 WinRows<>{nrm, s_nrm, lo});
 }
 
@@ -364,7 +378,7 @@ __global__ __launch_bounds__(256) void k_nvt1_list(GridView g, const float4* __r
     const int64_t n = (int64_t)*cnt;
     for (int64_t t = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x; t < n;
          t += (int64_t)gridDim.x * blockDim.x)
-        nvt1_row<K>(g, pos, nrm, idx, N, list[t], k, kstore, rho, tau, damp, cov, fn, err, Rows4{pos}, Rows4{nrm});
+        nvt1_row<K, false>(g, pos, nrm, idx, N, list[t], k, kstore, rho, tau, damp, cov, fn, err, Rows4{pos}, Rows4{nrm});
 }
 
 // Re-anchor: the exact KA nearest at the current position, one query per WAVE (pcd_wknn.h), capped by the old
@@ -421,6 +435,9 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
 }
 
 // K2: NVT2 on f_n -> classes + edge vectors.
+#ifndef PCD_NVT2_NORM
+#define PCD_NVT2_NORM false
+#endif
 template <int K>
 __global__ __launch_bounds__(256) void k_nvt2(const float4* __restrict__ pos, const float4* __restrict__ fn,
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
@@ -433,8 +450,10 @@ __global__ __launch_bounds__(256) void k_nvt2(const float4* __restrict__ pos, co
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 p4 = pos[i];
-    const Sym3 T = nvt_tensor<K>(WinRows<kWinHaloNvt2>{pos, s_pos, lo}, WinRows<kWinHaloNvt2>{fn, s_fn, lo}, v3(p4.x, p4.y, p4.z), k,
-                                 ColNbStream{idx, N, i}, rho, ColNbSafe{idx, N, i});
+    // classes and the edge vector are invariant to the positive scale 1/Σw (ratios of eigenvalues, a unit
+    // eigenvector): the tensor is left unnormalised.  f_n is NVT1's normalised output: the vote margin is constant.
+    const Sym3 T = nvt_tensor<K, PCD_NVT2_NORM, true>(WinRows<kWinHaloNvt2>{pos, s_pos, lo}, WinRows<kWinHaloNvt2>{fn, s_fn, lo},
+                                                v3(p4.x, p4.y, p4.z), k, ColNbStream{idx, N, i}, rho, ColNbSafe{idx, N, i});
 #ifdef PCD_NVT2_LAPACK
     float w[3], V[3][3];
     eigh3(T, w, V);
@@ -675,6 +694,7 @@ struct pcd_denoiser {
     hipEvent_t fork = nullptr, join = nullptr;
     int64_t last_dense = -1;      // rows of the last anchored stage when it re-anchored every row, else -1
     bool anchoring = true;        // anchored kNN for seeded searches (pcd_denoiser_set_anchoring)
+    bool unit_nrm = false;        // nrm holds the loop's own normalised f_n (set by finish, cleared by load / writes)
     int windows = 1;              // LDS row windows in NVT1 / NVT2 / the flat phase (pcd_denoiser_set_windows)
     bool loaded = false, iterated = false;
     bool timing = false;
@@ -796,7 +816,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
             if (overlap) {                                                                                             \
                 PCD_HIP(hipEventRecord(dn->fork, st));                                                                 \
                 PCD_HIP(hipStreamWaitEvent(dn->side, dn->fork, 0));                                                    \
-                hipLaunchKernelGGL((k_nvt1<C>), grd, blk, 0, dn->side, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,   \
+                hipLaunchKernelGGL((k_nvt1<C, false>), grd, blk, 0, dn->side, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,   \
                                    p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, dn->fail);          \
                 PCD_HIP(hipEventRecord(dn->join, dn->side));                                                           \
             }                                                                                                          \
@@ -812,9 +832,12 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
             hipLaunchKernelGGL((k_nvt1_list<C>), grd_list, blk, 0, st, gv, P, dn->nrm, dn->idx, N, p->k, kstore,       \
                                p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->redo, redo_cnt);                 \
             PCD_HIP(hipStreamWaitEvent(st, dn->join, 0));                                                              \
+        } else if (dn->unit_nrm) {                                                                                     \
+            hipLaunchKernelGGL((k_nvt1<C, true>), grd, blk, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,       \
+                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, nullptr);               \
         } else {                                                                                                       \
-            hipLaunchKernelGGL((k_nvt1<C>), grd, blk, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore, p->rho,     \
-                               p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, nullptr);                       \
+            hipLaunchKernelGGL((k_nvt1<C, false>), grd, blk, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,      \
+                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, nullptr);               \
         }                                                                                                              \
         break;
     switch (K) {
@@ -862,7 +885,9 @@ static int stage_k2(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t s
     const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
     float4* P = dn->pos[dn->cur];
 #define PCD_K2(C) \
-    case C: hipLaunchKernelGGL(k_nvt2<C>, grd, blk, 0, st, P, dn->fn, dn->idx, dn->n, rm, p->k, p->rho, p->class_scale, dn->cls, dn->edge, dn->windows); break;
+    case C:                                                                                                            \
+        hipLaunchKernelGGL((k_nvt2<C>), grd, blk, 0, st, P, dn->fn, dn->idx, dn->n, rm, p->k, p->rho, p->class_scale, dn->cls, dn->edge, dn->windows); \
+        break;
     switch (list_cap(p)) {
         PCD_K2(8) PCD_K2(16) PCD_K2(32) PCD_K2(64)
         default: return fail(PCD_ERR_ARG, "unsupported k");
@@ -950,6 +975,7 @@ static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, co
 static void stage_finish(pcd_denoiser* dn, const pcd_denoise_params* p) {
     if (p->jacobi && p->nphases > 0) dn->cur ^= 1;
     std::swap(dn->nrm, dn->fn);   // graph.n = f_n  (Processor.py:139)
+    dn->unit_nrm = true;
     dn->iterated = true;
 }
 
@@ -1018,6 +1044,7 @@ int pcd_denoiser_load(pcd_denoiser* dn, const float* pos, const float* n, void* 
     dn->cur = 0;
     dn->loaded = true;
     dn->iterated = false;
+    dn->unit_nrm = false;         // the caller's normals: the general vote margin until the first finish
     dn->seed_cols = 0;
     return PCD_OK;
 }
@@ -1066,6 +1093,7 @@ int pcd_denoiser_unpack(pcd_denoiser* dn, int field, const int32_t* rows, int64_
     hipLaunchKernelGGL(k_unpack, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, as_stream(stream), f, rows, n,
                        reinterpret_cast<const float4*>(in4));
     PCD_LAUNCH_CHECK();
+    if (field == PCD_FIELD_NRM) dn->unit_nrm = false;   // (FN rows must be another rank's NVT1 output: unit)
     return PCD_OK;
 }
 

@@ -71,6 +71,22 @@ struct RowMap {
 struct Sym3 { float a00, a01, a02, a11, a12, a22; };
 
 namespace lapack {
+// PCD_EIGH_FAST (experiment): the hardware reciprocal / square-root estimates (~1 ulp) in place of IEEE division and
+// sqrt inside the solver; the default build keeps LAPACK's IEEE arithmetic.
+PCD_DEV float ldiv(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PCD_EIGH_FAST)
+    return a * __builtin_amdgcn_rcpf(b);
+#else
+    return a / b;
+#endif
+}
+PCD_DEV float lsqrt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PCD_EIGH_FAST)
+    return __builtin_amdgcn_sqrtf(x);
+#else
+    return sqrtf(x);
+#endif
+}
 static constexpr float kEps = 5.9604644775390625e-08f;      // slamch('E') = 2^-24
 static constexpr float kSafmin = 1.17549435e-38f;          // slamch('S')
 static constexpr float kSafmn2 = 4.4408920985006262e-16f;  // 2^-51 (slartg scaling bounds)
@@ -81,8 +97,8 @@ PCD_DEV float slapy2(float x, float y) {
     const float xa = fabsf(x), ya = fabsf(y);
     const float w = fmaxf(xa, ya), z = fminf(xa, ya);
     if (z == 0.f || w > 3.4028235e38f) return w;
-    const float q = z / w;
-    return w * sqrtf(1.f + q * q);
+    const float q = ldiv(z, w);
+    return w * lsqrt(1.f + q * q);
 }
 // LAPACK <= 3.9 slartg: r = ±sqrt(f²+g²), c made positive only when |f| > |g|
 PCD_DEV void slartg(float f, float g, float& c, float& s, float& r) {
@@ -93,17 +109,17 @@ PCD_DEV void slartg(float f, float g, float& c, float& s, float& r) {
     int count = 0;
     if (scale >= kSafmx2) {
         do { f1 *= kSafmn2; g1 *= kSafmn2; ++count; } while (fmaxf(fabsf(f1), fabsf(g1)) >= kSafmx2 && count < 20);
-        r = sqrtf(f1 * f1 + g1 * g1);
-        c = f1 / r; s = g1 / r;
+        r = lsqrt(f1 * f1 + g1 * g1);
+        c = ldiv(f1, r); s = ldiv(g1, r);
         for (int i = 0; i < count; ++i) r *= kSafmx2;
     } else if (scale <= kSafmn2) {
         do { f1 *= kSafmx2; g1 *= kSafmx2; ++count; } while (fmaxf(fabsf(f1), fabsf(g1)) <= kSafmn2 && count < 20);
-        r = sqrtf(f1 * f1 + g1 * g1);
-        c = f1 / r; s = g1 / r;
+        r = lsqrt(f1 * f1 + g1 * g1);
+        c = ldiv(f1, r); s = ldiv(g1, r);
         for (int i = 0; i < count; ++i) r *= kSafmn2;
     } else {
-        r = sqrtf(f1 * f1 + g1 * g1);
-        c = f1 / r; s = g1 / r;
+        r = lsqrt(f1 * f1 + g1 * g1);
+        c = ldiv(f1, r); s = ldiv(g1, r);
     }
     if (fabsf(f) > fabsf(g) && c < 0.f) { c = -c; s = -s; r = -r; }
 }
@@ -113,24 +129,24 @@ PCD_DEV void slaev2(float a, float b, float c, float& rt1, float& rt2, float& cs
     float acmx, acmn;
     if (fabsf(a) > fabsf(c)) { acmx = a; acmn = c; } else { acmx = c; acmn = a; }
     float rt;
-    if (adf > ab) { const float q = ab / adf; rt = adf * sqrtf(1.f + q * q); }
-    else if (adf < ab) { const float q = adf / ab; rt = ab * sqrtf(1.f + q * q); }
+    if (adf > ab) { const float q = ldiv(ab, adf); rt = adf * lsqrt(1.f + q * q); }
+    else if (adf < ab) { const float q = ldiv(adf, ab); rt = ab * lsqrt(1.f + q * q); }
     else rt = ab * 1.41421356237309515f;
     int sgn1, sgn2;
-    if (sm < 0.f) { rt1 = 0.5f * (sm - rt); sgn1 = -1; rt2 = (acmx / rt1) * acmn - (b / rt1) * b; }
-    else if (sm > 0.f) { rt1 = 0.5f * (sm + rt); sgn1 = 1; rt2 = (acmx / rt1) * acmn - (b / rt1) * b; }
+    if (sm < 0.f) { rt1 = 0.5f * (sm - rt); sgn1 = -1; rt2 = ldiv(acmx, rt1) * acmn - ldiv(b, rt1) * b; }
+    else if (sm > 0.f) { rt1 = 0.5f * (sm + rt); sgn1 = 1; rt2 = ldiv(acmx, rt1) * acmn - ldiv(b, rt1) * b; }
     else { rt1 = 0.5f * rt; rt2 = -0.5f * rt; sgn1 = 1; }
     float cs;
     if (df >= 0.f) { cs = df + rt; sgn2 = 1; } else { cs = df - rt; sgn2 = -1; }
     if (fabsf(cs) > ab) {
-        const float ct = -tb / cs;
-        sn1 = 1.f / sqrtf(1.f + ct * ct);
+        const float ct = ldiv(-tb, cs);
+        sn1 = ldiv(1.f, lsqrt(1.f + ct * ct));
         cs1 = ct * sn1;
     } else if (ab == 0.f) {
         cs1 = 1.f; sn1 = 0.f;
     } else {
-        const float tn = -cs / tb;
-        cs1 = 1.f / sqrtf(1.f + tn * tn);
+        const float tn = ldiv(-cs, tb);
+        cs1 = ldiv(1.f, lsqrt(1.f + tn * tn));
         sn1 = tn * cs1;
     }
     if (sgn1 == sgn2) { const float tn = cs1; cs1 = -sn1; sn1 = tn; }
@@ -175,9 +191,9 @@ PCD_DEV void tail2(float d[3], float e[2], float Z[3][3]) {
 }
 PCD_DEV void ql_sweep3(float d[3], float e[2], float Z[3][3]) {   // l = 0, m = 2
     float p = d[0];
-    float g = (d[1] - p) / (2.f * e[0]);
+    float g = ldiv(d[1] - p, 2.f * e[0]);
     float r = slapy2(g, 1.f);
-    g = d[2] - p + (e[0] / (g + fsign(r, g)));
+    g = d[2] - p + ldiv(e[0], g + fsign(r, g));
     float s = 1.f, c = 1.f;
     p = 0.f;
     float f = s * e[1], b = c * e[1];
@@ -203,9 +219,9 @@ PCD_DEV void ql_sweep3(float d[3], float e[2], float Z[3][3]) {   // l = 0, m = 
 }
 PCD_DEV void qr_sweep3(float d[3], float e[2], float Z[3][3]) {   // l = 2, m = 0
     float p = d[2];
-    float g = (d[1] - p) / (2.f * e[1]);
+    float g = ldiv(d[1] - p, 2.f * e[1]);
     float r = slapy2(g, 1.f);
-    g = d[0] - p + (e[1] / (g + fsign(r, g)));
+    g = d[0] - p + ldiv(e[1], g + fsign(r, g));
     float s = 1.f, c = 1.f;
     p = 0.f;
     float f = s * e[0], b = c * e[0];
@@ -248,7 +264,7 @@ PCD_DEV void ssteqr3(float d[3], float e[2], float Z[3][3]) {
     auto split = [&](int mm) {
         const float tst = fabsf(e[mm]);
         if (tst == 0.f) return true;
-        if (tst <= (sqrtf(fabsf(d[mm])) * sqrtf(fabsf(d[mm + 1]))) * kEps) { e[mm] = 0.f; return true; }
+        if (tst <= (lsqrt(fabsf(d[mm])) * lsqrt(fabsf(d[mm + 1]))) * kEps) { e[mm] = 0.f; return true; }
         return false;
     };
     if (split(0)) {                       // blocks [0,0] [1,...]
@@ -477,8 +493,8 @@ PCD_DEV void eigh3(Sym3 A, float w[3], float V[3][3]) {
     float tau = 0.f, v2 = 0.f, e1 = a21;
     if (fabsf(a31) != 0.f) {
         const float beta = -fsign(slapy2(a21, fabsf(a31)), a21);
-        tau = (beta - a21) / beta;
-        v2 = a31 * (1.f / (a21 - beta));
+        tau = ldiv(beta - a21, beta);
+        v2 = a31 * ldiv(1.f, a21 - beta);
         e1 = beta;
         // x = tau * A22 * v (ssymv, lower), w = x - tau/2 (xᵀv) v, A22 -= v wᵀ + w vᵀ (ssyr2)
         float y1 = tau * a22;
@@ -593,14 +609,39 @@ PCD_DEV Vec3 vu_smooth(const float w[3], const float V[3][3], Vec3 n, float tau,
 // a cyclic Jacobi solve replaces the ssytd2 + ssteqr port: 4 fixed sweeps of the 3 plane rotations (fp32 Jacobi
 // converges quadratically; after 4 sweeps the off-diagonal is at rounding level), no data-dependent loop, no
 // divergence.  Eigenvalue error ~1e-7 of the trace (the tests' bound for eigenvalues is 2e-6).
+// On the device the rotation is built from the hardware reciprocal / square-root estimates (~1 ulp): any (c, s)
+// with c² + s² = 1 to rounding keeps the similarity orthogonal, and the off-diagonal still vanishes to rounding
+// after the fixed sweeps, so only the last bits of the eigenvalues change (PCD_NVT2_IEEE: the IEEE operations).
+PCD_DEV float jrcp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PCD_NVT2_IEEE)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.f / x;
+#endif
+}
+PCD_DEV float jsqrt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PCD_NVT2_IEEE)
+    return __builtin_amdgcn_sqrtf(x);
+#else
+    return sqrtf(x);
+#endif
+}
+PCD_DEV float jrsq(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PCD_NVT2_IEEE)
+    return __builtin_amdgcn_rsqf(x);
+#else
+    return 1.f / sqrtf(x);
+#endif
+}
 template <int P, int Q, int R>
 PCD_DEV void jacobi_rot(float (&a)[3][3], float (&V)[3][3]) {
     const float apq = a[P][Q];
-    const float theta = (a[Q][Q] - a[P][P]) / (2.f * apq);
-    float t = 1.f / (fabsf(theta) + sqrtf(theta * theta + 1.f));
+    const float theta = (a[Q][Q] - a[P][P]) * (0.5f * jrcp(apq));
+    float t = jrcp(fabsf(theta) + jsqrt(theta * theta + 1.f));
     t = theta < 0.f ? -t : t;
     t = apq == 0.f ? 0.f : t;                      // nothing to rotate (theta would be +-inf or NaN)
-    const float c = 1.f / sqrtf(t * t + 1.f), s = t * c;
+    t = t == t ? t : 0.f;                          // theta² overflowed to inf - inf: a negligible apq
+    const float c = jrsq(t * t + 1.f), s = t * c;
     a[P][P] = a[P][P] - t * apq;
     a[Q][Q] = a[Q][Q] + t * apq;
     a[P][Q] = a[Q][P] = 0.f;

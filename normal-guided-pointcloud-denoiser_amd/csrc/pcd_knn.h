@@ -187,7 +187,10 @@ PCD_DEV void knn_search(const GridView& g, Vec3 q, TopK<K>& tk, unsigned long lo
     while (!search_done(g, q, cx, cy, cz, R, tk.kth())) {
         ++R;
         PCD_KSTAT(tk, 5, 1);
-        if (R > 24) {  // pathological outlier: exhaustive scan (correct, slow, never hit on denoise inputs)
+        // A far outlier keeps growing Chebyshev shells (an empty cell costs one hash probe) until the block would
+        // hold more cells than the cloud has points -- only then is one exhaustive scan cheaper.
+        const int64_t side = 2 * (int64_t)R + 1;
+        if (R > 24 && side * side * side > (int64_t)g.n) {
             tk.init(cap);
             scan_range<K, ORIG>(g.pts, 0, (uint32_t)g.n, q, tk);
             return;

@@ -53,7 +53,13 @@ PCD_DEV void for_neighbours(P pos, Nr nrm, int cnt, Nb nb, F&& f) {
 // all-ones fallback (no vote) re-reads the rows and sums every n_j n_jᵀ in list order -- a rare row.
 // nbf: the same list for the rare fallback pass (a memory-backed accessor, so register-resident lists need not
 // stay live across the vote loop).
-template <int UNROLL = 0, class P, class Nr, class Nb, class NbF>
+// NORM = false: the sums without the division by Σ w (a positive scale: for callers that only need the
+// eigenvectors and scale-free ratios of the eigenvalues, NVT2's classes and edge vector).
+// UNIT = true: every n_j is a unit vector to rounding (|n_j| <= 1 + 1e-6, the kernels' own normalised f_n), so
+// (1 + |n_j|₁)² <= (1 + √3 (1 + 1e-6))² < 7.47 and the margin is the constant kUnitMargin·sq.
+static constexpr float kVoteEps = 4e-6f;
+static constexpr float kUnitMargin = kVoteEps * 7.47f;
+template <int UNROLL = 0, bool NORM = true, bool UNIT = false, class P, class Nr, class Nb, class NbF>
 PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF nbf) {
     float w00 = 0.f, w01 = 0.f, w02 = 0.f, w11 = 0.f, w12 = 0.f, w22 = 0.f;
     int wsum = 0;
@@ -68,11 +74,18 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF n
         const float sq = sq3(dv);
         const float e = (dv.x * nj.x + dv.y * nj.y) + dv.z * nj.z;
         const float lhs = e * e, rhs = cthr2 * sq;
-        const float n1 = 1.f + fabsf(nj.x) + fabsf(nj.y) + fabsf(nj.z);
-        bool w = lhs < rhs;
-        if (sq == 0.f) {
-            w = w_self;                      // the row itself (dv = 0): normalize gives 0, c = 0
-        } else if (!(fabsf(lhs - rhs) > 4e-6f * n1 * n1 * sq) || !(sq >= 1e-24f && sq < 1e30f)) {   // near: exact
+        float m;
+        if constexpr (UNIT) {
+            m = kUnitMargin * sq;
+        } else {
+            const float n1 = 1.f + fabsf(nj.x) + fabsf(nj.y) + fabsf(nj.z);
+            m = kVoteEps * n1 * n1 * sq;
+        }
+        // one rarely taken branch per neighbour: the pairs within the margin (or outside the safe range of sq)
+        // evaluate the reference expression; sq = 0 (the row itself) has the constant vote and is never "near"
+        const bool near = sq != 0.f && (!(fabsf(lhs - rhs) > m) || !(sq >= 1e-24f && sq < 1e30f));
+        bool w = sq == 0.f ? w_self : lhs < rhs;
+        if (near) {
             const float den = fmaxf(sqrtf(sq), 1e-12f);
             const Vec3 dn = v3(dv.x / den, dv.y / den, dv.z / den);
             float c = dot3(dn, nj);
@@ -96,6 +109,7 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF n
         }
         wsum = cnt;
     }
+    if (!NORM) return Sym3{w00, w01, w02, w11, w12, w22};
     const float c = (float)wsum;
     return Sym3{w00 / c, w01 / c, w02 / c, w11 / c, w12 / c, w22 / c};
 }

@@ -520,3 +520,20 @@ def test_large_cloud_knn_exact_vs_bruteforce(gpu):
     kth = torch.topk(bf, 32, largest=False).values[:, -1].float()
     np.testing.assert_allclose(d2[:, -1].cpu().numpy(), kth.cpu().numpy(), rtol=1e-4, atol=1e-9)
     assert (idx >= 0).all() and (idx < N).all()
+
+
+def test_large_cloud_far_queries_keep_growing_shells(gpu):
+    """Queries tens of cells off a 1M-point sheet: the Chebyshev shells keep growing past R = 24 (no exhaustive
+    O(N) fallback until the block outgrows the cloud) and the k-th distances stay exact (torch brute force checks)."""
+    g = torch.Generator(device=gpu).manual_seed(1)
+    N = 1_000_000
+    pos = torch.rand((N, 3), generator=g, device=gpu)
+    pos[:, 2] = 0.001 * pos[:, 2]                                   # a thin sheet: cell ~ 1/180 of its side
+    grid = nat.Grid(pos, k_hint=32)
+    q = torch.rand((256, 3), generator=g, device=gpu)
+    q[:, 2] = torch.linspace(0.05, 0.6, 256, device=gpu)            # 9 .. 110 cells above the sheet
+    idx, d2 = grid.knn(q, 8, with_d2=True)
+    bf = torch.cdist(q.double(), pos.double()) ** 2
+    ref = torch.topk(bf, 8, largest=False)
+    np.testing.assert_allclose(d2.cpu().numpy(), ref.values.float().cpu().numpy(), rtol=1e-5, atol=1e-9)
+    assert (idx == ref.indices).float().mean() > 0.999

@@ -9,6 +9,7 @@ usage: python tools/pmc_traffic.py <fetch counter_collection.csv> <write counter
 import csv
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -51,13 +52,14 @@ def main():
     # bytes of one seeded iteration: every per-iteration kernel's average bytes x its launches, over the number of
     # iterations (= NVT2 launches); one-time kernels (grid build, load/store, the dense first re-anchoring) excluded
     one_time = ("k_bbox", "k_sample", "k_keys", "k_gather_sorted", "k_count_starts", "k_brick_flags", "k_insert",
-                "k_load", "k_store", "k_edge_len", "k_knn<", "k_nn1", "k_radius", "true>")
-    n_iter = sum(e["launches_fetch"] for e in kernels.get("k_nvt2<32>", [])) or None
+                "k_load", "k_store", "k_edge_len", "k_knn<", "k_nn1", "k_radius")
+    dense = re.compile(r"k_knn_(redo_wave|requery|nvt1)<\d+, true")   # the dense first re-anchoring / unseeded K1
+    n_iter = sum(e["launches_fetch"] for kn, v in kernels.items() if kn.startswith("k_nvt2<32") for e in v) or None
     per_iter = None
     if n_iter:
         per_iter = 0.0
         for kname, v in kernels.items():
-            if any(t in kname for t in one_time):
+            if any(t in kname for t in one_time) or dense.search(kname):
                 continue
             for e in v:
                 if e.get("hbm_bytes_per_launch") is not None:
