@@ -189,6 +189,19 @@ PCD_DEV void tail2(float d[3], float e[2], float Z[3][3]) {
     rot_cols_c(Z, J, c, s);
     d[J] = rt1; d[J + 1] = rt2; e[J] = 0.f;
 }
+// tail2<0> / tail2<1> with the block chosen at run time (J1: [1,2]): one slaev2 for a wave whose lanes differ
+PCD_DEV void tail2r(bool J1, float d[3], float e[2], float Z[3][3]) {
+    float rt1, rt2, c, s;
+    slaev2(J1 ? d[1] : d[0], J1 ? e[1] : e[0], J1 ? d[2] : d[1], rt1, rt2, c, s);
+    const bool id = (c == 1.f && s == 0.f);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float t = J1 ? Z[i][2] : Z[i][1], z = J1 ? Z[i][1] : Z[i][0];
+        const float n1 = id ? t : c * t - s * z, n0 = id ? z : s * t + c * z;
+        if (J1) { Z[i][2] = n1; Z[i][1] = n0; } else { Z[i][1] = n1; Z[i][0] = n0; }
+    }
+    if (J1) { d[1] = rt1; d[2] = rt2; e[1] = 0.f; } else { d[0] = rt1; d[1] = rt2; e[0] = 0.f; }
+}
 PCD_DEV void ql_sweep3(float d[3], float e[2], float Z[3][3]) {   // l = 0, m = 2
     float p = d[0];
     float g = ldiv(d[1] - p, 2.f * e[0]);
@@ -278,40 +291,43 @@ PCD_DEV void ssteqr3(float d[3], float e[2], float Z[3][3]) {
         float anorm = fmaxf(fmaxf(fmaxf(0.f, fabsf(d[0])), fabsf(d[1])), fabsf(d[2]));
         anorm = fmaxf(fmaxf(anorm, fabsf(e[0])), fabsf(e[1]));
         if (anorm != 0.f) {
-            int jtot = 0;
-            if (!(fabsf(d[2]) < fabsf(d[0]))) {
-                // QL from the top: l = 0 until e[0] or e[1] deflates, then the 2x2 tail [1,2] or [0,1]
-                int l = 0;
-                for (;;) {
-                    if (l == 0) {
-                        if (ql_small(e[0], d[0], d[1])) { e[0] = 0.f; l = 1; continue; }
-                        if (ql_small(e[1], d[1], d[2])) { e[1] = 0.f; tail2<0>(d, e, Z); break; }
-                        if (jtot == nmaxit) break;
-                        ++jtot;
-                        ql_sweep3(d, e, Z);
-                    } else {                  // l == 1: block [1,2]
-                        if (ql_small(e[1], d[1], d[2])) e[1] = 0.f;
-                        else tail2<1>(d, e, Z);
-                        break;
-                    }
-                }
-            } else {
-                // QR from the bottom: l = 2 until e[1] or e[0] deflates, then the tail [0,1] or [1,2]
-                int l = 2;
-                for (;;) {
-                    if (l == 2) {
-                        if (ql_small(e[1], d[2], d[1])) { e[1] = 0.f; l = 1; continue; }
-                        if (ql_small(e[0], d[1], d[0])) { e[0] = 0.f; tail2<1>(d, e, Z); break; }
-                        if (jtot == nmaxit) break;
-                        ++jtot;
-                        qr_sweep3(d, e, Z);
-                    } else {                  // l == 1: block [0,1]
-                        if (ql_small(e[0], d[1], d[0])) e[0] = 0.f;
-                        else tail2<0>(d, e, Z);
-                        break;
-                    }
+            // LAPACK picks QL from the top, or QR from the bottom when |d[2]| < |d[0]|.  QR on (d, e, Z) is QL on the
+            // reversed problem (d0 <-> d2, e0 <-> e1, Z's columns reversed) operation for operation -- the same
+            // deflation tests on the same operands, the same sweep arithmetic (the rotations' sign conventions
+            // mirror), so every lane runs ONE loop in its own frame instead of a wave running both loops.  Only the
+            // 2x2 tail (slaev2's operand order) is frame-specific: it runs after the way back.
+            const bool qr = fabsf(d[2]) < fabsf(d[0]);
+            float fd[3] = {qr ? d[2] : d[0], d[1], qr ? d[0] : d[2]};
+            float fe[2] = {qr ? e[1] : e[0], qr ? e[0] : e[1]};
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) Z[i][j] = (qr ? (i + j == 2) : (i == j)) ? 1.f : 0.f;   // Z J or Z
+            int tail = 0;                     // 1: the frame's block [1,2] needs slaev2, 2: its block [0,1]
+            int jtot = 0, l = 0;
+            for (;;) {
+                if (l == 0) {
+                    if (ql_small(fe[0], fd[0], fd[1])) { fe[0] = 0.f; l = 1; continue; }
+                    if (ql_small(fe[1], fd[1], fd[2])) { fe[1] = 0.f; tail = 2; break; }
+                    if (jtot == nmaxit) break;
+                    ++jtot;
+                    ql_sweep3(fd, fe, Z);
+                } else {                      // l == 1: the frame's block [1,2]
+                    if (ql_small(fe[1], fd[1], fd[2])) fe[1] = 0.f;
+                    else tail = 1;
+                    break;
                 }
             }
+            d[0] = qr ? fd[2] : fd[0]; d[1] = fd[1]; d[2] = qr ? fd[0] : fd[2];
+            e[0] = qr ? fe[1] : fe[0]; e[1] = qr ? fe[0] : fe[1];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const float z0 = Z[i][0], z2 = Z[i][2];
+                Z[i][0] = qr ? z2 : z0;
+                Z[i][2] = qr ? z0 : z2;
+            }
+            // the frame's [1,2] is the original [1,2] (QL) or [0,1] (QR); its [0,1] the original [0,1] or [1,2]
+            if (tail != 0) tail2r((tail == 1) != qr, d, e, Z);
         }
     }
     // selection sort, ascending (swaps columns of Z)
