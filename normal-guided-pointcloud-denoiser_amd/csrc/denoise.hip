@@ -340,7 +340,8 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
             if (t == kstore - 1) dk = dist2(vi, g.pts[l[t]]);
         if (!cov.holds(vi, dk)) atomicOr(err, 2);
     }
-    const Sym3 T = nvt_tensor<K, true, UNIT>(rp, rn, vi, k, RegNb32{l}, rho, ColNbSafe{idx, N, i});
+    // 4 neighbours in flight per batch (8 measured 0.06 ms slower at 10M: the VGPRs of 8 rows in flight)
+    const Sym3 T = nvt_tensor<K, true, UNIT, 4>(rp, rn, vi, k, RegNb32{l}, rho, ColNbSafe{idx, N, i});
     float w[3], V[3][3];
     eigh3(T, w, V);
     const float4 n4 = nrm[i];
@@ -352,8 +353,11 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
 // run on a side stream while the re-anchoring search works on the others (pcd_denoiser::side).
 // UNIT: the normals are the loop's own normalised f_n (every iteration after the first since load): the vote's
 // margin is a constant (nvt_tensor).
+#ifndef PCD_NVT1_OCC
+#define PCD_NVT1_OCC 1
+#endif
 template <int K, bool UNIT>
-__global__ __launch_bounds__(256) void k_nvt1(GridView g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
+__global__ __launch_bounds__(256, PCD_NVT1_OCC) void k_nvt1(GridView g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                int kstore, float rho, float tau, float damp, Cover cov,
                                                float4* __restrict__ fn, int* __restrict__ err, int win,
@@ -622,10 +626,10 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
         o = step_flat<KU>(WinRows<kWinHaloPhase>{pin, s_pos, lo}, WinRows<kWinHaloPhase>{fn, s_fn, lo}, vi, F(i), ku, nb,
                           __uint_as_float(((const unsigned*)g)[3]), d, alpha);
     else if (KIND == PCD_STEP_FLAT) o = step_flat<KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
-    else if (KIND == PCD_STEP_EDGE) o = step_edge<KU>(P, F, vi, Rows4{edge}(i), ku, nb, d, alpha);
-    else if (KIND == PCD_STEP_FEATURE) o = step_feature<false, KU>(P, F, vi, F(i), ku, nb, 1.f, d, alpha);
+    else if (KIND == PCD_STEP_EDGE) o = step_edge<KU, 4>(P, F, vi, Rows4{edge}(i), ku, nb, d, alpha);
+    else if (KIND == PCD_STEP_FEATURE) o = step_feature<false, KU, 4>(P, F, vi, F(i), ku, nb, 1.f, d, alpha);
     else if (KIND == PCD_STEP_NEW) o = step_feature<true, KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
-    else if (KIND == PCD_STEP_CORNER) o = step_corner<KU>(P, F, vi, ku, nb, d, alpha);
+    else if (KIND == PCD_STEP_CORNER) o = step_corner<KU, 4>(P, F, vi, ku, nb, d, alpha);
     else o = vi;
     if (clampg > 0.f) {                 // global clamp against the loaded positions (PostProcessing.ipynb:1088-1089)
         const float4 o4 = orig[i];

@@ -6,20 +6,23 @@
 
 namespace pcd {
 
-static constexpr int kNbBatch = 8;   // neighbours gathered together (every load of a batch in flight)
+#ifndef PCD_NB_BATCH
+#define PCD_NB_BATCH 8
+#endif
+static constexpr int kNbBatch = PCD_NB_BATCH;   // neighbours gathered together (every load of a batch in flight)
 
 // Neighbour loop of a fused kernel: M = compile-time bound on cnt (list cap).  The list entries are read first, then
 // the neighbours' (v_j, n_j) in batches of kNbBatch whose loads are all issued before any is consumed; f(vj, nj) runs
 // for t < cnt in list order, so every sum keeps the reference's summation order.  M = 0: plain runtime loop.
-template <int M, class P, class Nr, class Nb, class F>
+template <int M, int BATCH = kNbBatch, class P, class Nr, class Nb, class F>
 PCD_DEV void for_neighbours(P pos, Nr nrm, int cnt, Nb nb, F&& f) {
     if constexpr (M > 0) {
         int32_t jj[M];
 #pragma unroll
         for (int t = 0; t < M; ++t) jj[t] = (int32_t)nb(t < cnt ? t : cnt - 1);
 #pragma unroll
-        for (int b = 0; b < M; b += kNbBatch) {
-            constexpr int B = M < kNbBatch ? M : kNbBatch;
+        for (int b = 0; b < M; b += BATCH) {
+            constexpr int B = M < BATCH ? M : BATCH;
             Vec3 vb[B], nv[B];
 #pragma unroll
             for (int u = 0; u < B; ++u) { vb[u] = pos(jj[b + u]); nv[u] = nrm(jj[b + u]); }
@@ -59,7 +62,8 @@ PCD_DEV void for_neighbours(P pos, Nr nrm, int cnt, Nb nb, F&& f) {
 // (1 + |n_j|₁)² <= (1 + √3 (1 + 1e-6))² < 7.47 and the margin is the constant kUnitMargin·sq.
 static constexpr float kVoteEps = 4e-6f;
 static constexpr float kUnitMargin = kVoteEps * 7.47f;
-template <int UNROLL = 0, bool NORM = true, bool UNIT = false, class P, class Nr, class Nb, class NbF>
+template <int UNROLL = 0, bool NORM = true, bool UNIT = false, int BATCH = kNbBatch, class P, class Nr, class Nb,
+          class NbF>
 PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF nbf) {
     float w00 = 0.f, w01 = 0.f, w02 = 0.f, w11 = 0.f, w12 = 0.f, w22 = 0.f;
     int wsum = 0;
@@ -98,7 +102,7 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF n
         w11 += nw.y * nj.y; w12 += nw.y * nj.z; w22 += nw.z * nj.z;
         wsum += w ? 1 : 0;
     };
-    for_neighbours<UNROLL>(pos, nrm, cnt, nb, body2);
+    for_neighbours<UNROLL, BATCH>(pos, nrm, cnt, nb, body2);
     if (wsum == 0) {
         w00 = w01 = w02 = w11 = w12 = w22 = 0.f;
 #pragma unroll 1
@@ -248,13 +252,13 @@ PCD_DEV Vec3 step_flat(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float de
 }
 
 // ----------------------------------------------------------------- H10: Denoiser.edge_step (Denoiser.py:53-88)
-template <int M = 0, class P, class Nr, class Nb>
+template <int M = 0, int BATCH = kNbBatch, class P, class Nr, class Nb>
 PCD_DEV Vec3 step_edge(P pos, Nr nrm, Vec3 vi, Vec3 y, int cnt, Nb nb, float d, float alpha) {
     float A[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
     Vec3 b = v3(0.f, 0.f, 0.f);
     const Vec3 yyvi = outer_mul(y, vi);
     const float yc[3] = {y.x, y.y, y.z};
-    for_neighbours<M>(pos, nrm, cnt, nb, [&](const Vec3 vj, const Vec3 nj) {
+    for_neighbours<M, BATCH>(pos, nrm, cnt, nb, [&](const Vec3 vj, const Vec3 nj) {
         const Vec3 vjp = vj - dot3(vj - vi, y) * y;
         const Vec3 njp = nj - dot3(nj, y) * y;
         const float nc[3] = {njp.x, njp.y, njp.z};
@@ -271,13 +275,13 @@ PCD_DEV Vec3 step_edge(P pos, Nr nrm, Vec3 vi, Vec3 y, int cnt, Nb nb, float d, 
 
 // ----------------------------------------------------------------- H11: Denoiser.feature_step (Denoiser.py:174-219)
 //                                 and H12: Denoiser.new_step (Denoiser.py:121-172; WEIGHTED=true)
-template <bool WEIGHTED, int M = 0, class P, class Nr, class Nb>
+template <bool WEIGHTED, int M = 0, int BATCH = kNbBatch, class P, class Nr, class Nb>
 PCD_DEV Vec3 step_feature(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float delta, float d, float alpha) {
     float S[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};  // Σ w nj njᵀ
     Vec3 svj = v3(0.f, 0.f, 0.f);                                       // Σ w vj
     Vec3 snv = v3(0.f, 0.f, 0.f);                                       // Σ w (nj njᵀ) vj
     const float dd = delta * delta;
-    for_neighbours<M>(pos, nrm, cnt, nb, [&](const Vec3 vj, const Vec3 nj) {
+    for_neighbours<M, BATCH>(pos, nrm, cnt, nb, [&](const Vec3 vj, const Vec3 nj) {
         float w = 1.f;
         if (WEIGHTED) {
             const float dt = dot3(nj, vj - vi);
@@ -309,11 +313,11 @@ PCD_DEV Vec3 step_feature(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float
 }
 
 // ----------------------------------------------------------------- H12: Denoiser.corner_step (Denoiser.py:26-51)
-template <int M = 0, class P, class Nr, class Nb>
+template <int M = 0, int BATCH = kNbBatch, class P, class Nr, class Nb>
 PCD_DEV Vec3 step_corner(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float d, float alpha) {
     float A[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
     Vec3 b = v3(0.f, 0.f, 0.f);
-    for_neighbours<M>(pos, nrm, cnt, nb, [&](const Vec3 vj, const Vec3 nj) {
+    for_neighbours<M, BATCH>(pos, nrm, cnt, nb, [&](const Vec3 vj, const Vec3 nj) {
         add_outer(A, nj);
         b = b + outer_mul(nj, vj);
     });
