@@ -72,10 +72,10 @@ def knn_cap(k):
 def k1_kernels(k, ku, seeding, anchoring):
     """Kernels of the K1 stage (kNN + NVT1) as pcd_denoiser_iterate launches them in a timed (seeded) step."""
     c = knn_cap(max(k, ku))
-    full = "false"   # k_nvt1's compile-time list length (PCD_NVT_FULL) is off in the product build
+    unit = "true"    # k_nvt1<C, UNIT>: every timed iteration runs on the loop's own unit normals
     if seeding and anchoring and c <= 32:
         return [f"k_knn_anchor<{c}, {2 * c}>", f"k_knn_requery<{2 * c}, false, 64>", f"k_knn_redo_wave<{2 * c}, false>",
-                f"k_nvt1<{c}, {full}>"]
+                f"k_nvt1<{c}, {unit}>"]
     return [f"k_knn_nvt1<{c}, {'true' if seeding else 'false'}>"]
 
 

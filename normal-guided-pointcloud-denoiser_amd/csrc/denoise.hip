@@ -812,7 +812,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
         if (dense) {                                                                                                   \
             if (ev) PCD_HIP(hipEventRecord(ev[1], st));                                                                \
             hipLaunchKernelGGL((k_knn_requery<2 * C, true>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, PCD_RQ_RDENSE,   \
-                               dn->anc, dn->alist, dn->idx, dn->redo, redo_cnt, dn->spill, spill_cnt);                 \
+                               dn->anc, dn->alist, dn->idx, nullptr, nullptr, dn->spill, spill_cnt);                   \
         } else {                                                                                                       \
             hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd_anc, dim3(kAnchorBS), 0, st, gv, P, N, rm, kstore,        \
                                dn->anc, dn->alist, dn->idx, dn->fail);                                                 \

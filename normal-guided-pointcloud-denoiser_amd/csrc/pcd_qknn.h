@@ -240,41 +240,31 @@ struct RqCells {            // per-group LDS scratch for one chunk of cells
     uint32_t start[kRqChunk];
     uint32_t end_incl[kRqChunk];
 };
-template <int K, int W>
-PCD_DEV bool rq_scan_box(const GridView& g, Vec3 q, const int lo[3], const int hi[3], unsigned long long& cap,
-                         unsigned long long* buf, int& cnt, RqCells* wc, const LaneGrp<W>& lg) {
-    constexpr int CPL = RqCPL<W>::n;
-    static_assert(CPL >= 1 && CPL * W == kRqChunk, "chunk = whole cells per lane");
-    static_assert(K + W * kRqRows <= RqSurv<W>::n, "a cut to K plus one round of appends must fit the buffer");
-    const int hl = lg.hl;
-    const int ex = hi[0] - lo[0] + 1, ey = hi[1] - lo[1] + 1;
-    const int nc = ex * ey * (hi[2] - lo[2] + 1);
-    const uint32_t exy = (uint32_t)ex * (uint32_t)ey;
-    for (int base = 0; base < nc; base += kRqChunk) {
+// Where a scan reads its cells and candidate rows from: GridSrc is the grid in global memory (brick hash probes,
+// brick cell blocks, snapshot rows; a row's rank is its index).  A source only has to resolve a lane's cells to row
+// ranges, load a row with its rank, and say whether it covers a cell box (an LDS-staged brick neighbourhood was
+// measured this way: DESIGN §3).
+struct GridSrc {
+    const GridView* g;
+    template <int CPL>
+    PCD_DEV void ranges(const int (&cx)[CPL], const int (&cy)[CPL], const int (&cz)[CPL], const bool (&on)[CPL],
+                        uint2 (&cr)[CPL]) const {
         uint32_t slot[CPL], loc6[CPL];
         unsigned long long bkey[CPL];
-        const float kth = __uint_as_float((unsigned)(cap >> 32));
 #pragma unroll
         for (int u = 0; u < CPL; ++u) {
-            const uint32_t ci = (uint32_t)(base + hl * CPL + u);
             slot[u] = ~0u; loc6[u] = 0; bkey[u] = kEmptyKey;
-            if (ci < (uint32_t)nc) {
-                const uint32_t zq = ci / exy, rem = ci - zq * exy, yq = rem / (uint32_t)ex;
-                const int cx = lo[0] + (int)(rem - yq * (uint32_t)ex), cy = lo[1] + (int)yq, cz = lo[2] + (int)zq;
-                const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
-                const float gx = axis_gap(q.x, lx, lx + g.h), gy = axis_gap(q.y, ly, ly + g.h), gz = axis_gap(q.z, lz, lz + g.h);
-                if (gx * gx + gy * gy + gz * gz <= kth * 1.00001f + 1e-30f) {
-                    const unsigned long long key = morton3(cx, cy, cz);
-                    bkey[u] = key >> 6;
-                    loc6[u] = (uint32_t)(key & 63);
-                    slot[u] = (uint32_t)hash_slot(bkey[u], g.hbits);
-                }
+            if (on[u]) {
+                const unsigned long long key = morton3(cx[u], cy[u], cz[u]);
+                bkey[u] = key >> 6;
+                loc6[u] = (uint32_t)(key & 63);
+                slot[u] = (uint32_t)hash_slot(bkey[u], g->hbits);
             }
         }
         uint4 sl[CPL];
 #pragma unroll
         for (int u = 0; u < CPL; ++u)
-            sl[u] = slot[u] != ~0u ? *reinterpret_cast<const uint4*>(g.table + slot[u]) : make_uint4(~0u, ~0u, 0u, 0u);
+            sl[u] = slot[u] != ~0u ? *reinterpret_cast<const uint4*>(g->table + slot[u]) : make_uint4(~0u, ~0u, 0u, 0u);
         uint32_t brick[CPL];
 #pragma unroll
         for (int u = 0; u < CPL; ++u) {
@@ -286,14 +276,53 @@ PCD_DEV bool rq_scan_box(const GridView& g, Vec3 q, const int lo[3], const int h
                 const unsigned long long k2 = (unsigned long long)e.x | ((unsigned long long)e.y << 32);
                 if (k2 == bkey[u]) { brick[u] = e.z; break; }
                 if (k2 == kEmptyKey) break;
-                sidx = (uint32_t)((sidx + 1) & g.mask);
-                e = *reinterpret_cast<const uint4*>(g.table + sidx);
+                sidx = (uint32_t)((sidx + 1) & g->mask);
+                e = *reinterpret_cast<const uint4*>(g->table + sidx);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < CPL; ++u)
+            cr[u] = brick[u] != ~0u ? g->cells[(uint64_t)brick[u] * 64 + loc6[u]] : make_uint2(0u, 0u);
+    }
+    PCD_DEV void row(uint32_t r, float& x, float& y, float& z, uint32_t& rank) const {
+        const float* pp = reinterpret_cast<const float*>(g->pts + r);
+        x = pp[0]; y = pp[1]; z = pp[2]; rank = r;
+    }
+    PCD_DEV bool covers(const int (&)[3], const int (&)[3]) const { return true; }
+};
+
+// Scan the cells of box [lo, hi] (at most kRqMaxCells) appending keys < cap to buf: pcd_wknn.h wave_scan_box
+// in 32-bit cell arithmetic, with the quantised buffer cut, for one lane group.  Returns false when a cut was
+// ambiguous (spill).
+template <int K, int W, class Src>
+PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo[3], const int hi[3],
+                         unsigned long long& cap, unsigned long long* buf, int& cnt, RqCells* wc, const LaneGrp<W>& lg) {
+    constexpr int CPL = RqCPL<W>::n;
+    static_assert(CPL >= 1 && CPL * W == kRqChunk, "chunk = whole cells per lane");
+    static_assert(K + W * kRqRows <= RqSurv<W>::n, "a cut to K plus one round of appends must fit the buffer");
+    const int hl = lg.hl;
+    const int ex = hi[0] - lo[0] + 1, ey = hi[1] - lo[1] + 1;
+    const int nc = ex * ey * (hi[2] - lo[2] + 1);
+    const uint32_t exy = (uint32_t)ex * (uint32_t)ey;
+    for (int base = 0; base < nc; base += kRqChunk) {
+        int cxs[CPL], cys[CPL], czs[CPL];
+        bool on[CPL];
+        const float kth = __uint_as_float((unsigned)(cap >> 32));
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const uint32_t ci = (uint32_t)(base + hl * CPL + u);
+            on[u] = false; cxs[u] = cys[u] = czs[u] = 0;
+            if (ci < (uint32_t)nc) {
+                const uint32_t zq = ci / exy, rem = ci - zq * exy, yq = rem / (uint32_t)ex;
+                const int cx = lo[0] + (int)(rem - yq * (uint32_t)ex), cy = lo[1] + (int)yq, cz = lo[2] + (int)zq;
+                const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
+                const float gx = axis_gap(q.x, lx, lx + g.h), gy = axis_gap(q.y, ly, ly + g.h), gz = axis_gap(q.z, lz, lz + g.h);
+                on[u] = gx * gx + gy * gy + gz * gz <= kth * 1.00001f + 1e-30f;
+                cxs[u] = cx; cys[u] = cy; czs[u] = cz;
             }
         }
         uint2 cr[CPL];
-#pragma unroll
-        for (int u = 0; u < CPL; ++u)
-            cr[u] = brick[u] != ~0u ? g.cells[(uint64_t)brick[u] * 64 + loc6[u]] : make_uint2(0u, 0u);
+        src.template ranges<CPL>(cxs, cys, czs, on, cr);
         uint32_t loc[CPL], run = 0;
 #pragma unroll
         for (int u = 0; u < CPL; ++u) {
@@ -330,19 +359,17 @@ PCD_DEV bool rq_scan_box(const GridView& g, Vec3 q, const int lo[3], const int h
                 r[u] = j < total ? wc->start[a] + (j - (a ? wc->end_incl[a - 1] : 0u)) : 0u;
             }
             float px[kRqRows], py[kRqRows], pz[kRqRows];
+            uint32_t rk[kRqRows];
 #pragma unroll
             for (int u = 0; u < kRqRows; ++u) {
-                if (j0 + (uint32_t)(u * W) < total) {
-                    const float* pp = reinterpret_cast<const float*>(g.pts + r[u]);
-                    px[u] = pp[0]; py[u] = pp[1]; pz[u] = pp[2];
-                }
+                if (j0 + (uint32_t)(u * W) < total) src.row(r[u], px[u], py[u], pz[u], rk[u]);
             }
 #pragma unroll
             for (int u = 0; u < kRqRows; ++u) {
                 const uint32_t j = j0 + (uint32_t)(u * W + hl);
                 if (j0 + (uint32_t)(u * W) < total) {
                     const unsigned long long key2 =
-                        ((unsigned long long)__float_as_uint(dist2(q, make_float4(px[u], py[u], pz[u], 0.f))) << 32) | r[u];
+                        ((unsigned long long)__float_as_uint(dist2(q, make_float4(px[u], py[u], pz[u], 0.f))) << 32) | rk[u];
                     const bool pass = j < total && key2 < cap;
                     const unsigned long long m = lg.ballot(pass);
                     if (pass) buf[cnt + __popcll(m & ((1ull << hl) - 1ull))] = key2;
@@ -365,6 +392,86 @@ struct RqStats { unsigned redo_cnt, spill_cnt, spill_big, spill_amb; };
 #ifndef PCD_RQ_OCC
 #define PCD_RQ_OCC 8
 #endif
+// One re-anchoring query (the rows of a lane group; q, i uniform in the group): the exact anchor set within radius
+// r_s (widened x 1.6 up to twice while it holds at most kstore points), the stored list, the new anchor.  Spills an
+// ambiguous or oversized query to the exact-key wave search.  Returns false, having written nothing, when a box
+// leaves what `src` covers (StagedSrc: the caller hands the query to the global-memory pass).
+template <int KA, int W, class Src>
+PCD_DEV bool rq_query(const GridView& g, const Src& src, int64_t i, Vec3 q, float r_s, int64_t N, int kstore,
+                      float4* __restrict__ anc, int32_t* __restrict__ alist, int32_t* __restrict__ idx,
+                      int32_t* __restrict__ spill, unsigned* __restrict__ spill_cnt, unsigned long long* buf,
+                      RqCells* wc, const LaneGrp<W>& lg) {
+    unsigned long long cap = 0;
+    int cnt = 0;
+    bool big = false, ok = false;
+    // a radius holding at most kstore points is widened (x 1.6, twice) before the query spills
+#pragma unroll 1
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        if (attempt > 0) r_s *= 1.6f;
+        cap = ((unsigned long long)__float_as_uint(r_s * r_s) << 32) | 0xFFFFFFFFull;
+        const float rr = r_s * 1.0001f + 1e-30f;
+        int lo[3], hi[3];
+        cell_box(g, q, rr, lo, hi);
+        cnt = 0;
+        const int64_t nbox = (int64_t)(hi[0] - lo[0] + 1) * (hi[1] - lo[1] + 1) * (hi[2] - lo[2] + 1);
+        big = nbox > kRqMaxCells;
+        if (big) break;
+        if (!src.covers(lo, hi)) return false;    // (block-uniform per query: every lane of the group)
+        const bool clean = rq_scan_box<KA, W>(g, src, q, lo, hi, cap, buf, cnt, wc, lg);
+        ok = clean && cnt > kstore;
+        if (ok || !clean) break;
+        wave_sync();
+    }
+    const bool partial = cnt < KA;               // (after a buffer cut cnt == KA)
+    GrpOrder<W> o{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, &lg};
+    if (ok) {
+        (void)rq_shrink<KA, W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lg);
+        ok = cnt <= 4 * W;                        // (a set that did not shrink to 4W spills)
+    }
+    if (ok) {
+        o = grp_order32<W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lg);
+        // exact order of the stored list (first kstore + its successor) and of the anchor set boundary
+        ok = order_exact<W>(o, kstore, lg);
+        ok = ok && (cnt <= KA || (o.at(KA) >> 8) != (o.at(KA - 1) >> 8));
+    }
+    if (!ok) {
+        wave_sync();
+        if (lg.hl == 0) {
+            spill[atomicAdd(spill_cnt, 1u)] = (int32_t)i;
+            atomicAdd(big ? spill_cnt + 1 : spill_cnt + 2, 1u);   // RqStats::spill_big / spill_amb
+        }
+        return true;
+    }
+    // this lane's elements hl and W + hl of the order; unused slots of a partial set hold -1 (the anchor test
+    // gives them an infinite distance)
+    const int e0 = lg.hl, e1 = W + lg.hl;
+    const bool h0 = e0 < KA && e0 < cnt, h1 = e1 < KA && e1 < cnt;
+    const unsigned long long m0 = h0 ? buf[o.s0 & 255u] : 0ull;
+    const unsigned long long m1 = h1 ? buf[o.s1 & 255u] : 0ull;
+    const int32_t r0 = h0 ? (int32_t)(uint32_t)(m0 & 0xFFFFFFFFull) : -1;
+    const int32_t r1 = h1 ? (int32_t)(uint32_t)(m1 & 0xFFFFFFFFull) : -1;
+    if (e0 < kstore) idx[(int64_t)e0 * N + i] = r0;
+    if (e1 < kstore) idx[(int64_t)e1 * N + i] = r1;
+    // the anchor set is stored in RANK order (unused slots last): the anchor test ranks it by distance itself,
+    // and neighbouring rows -- neighbouring lanes of its waves -- then gather nearly the same snapshot rows in the
+    // same slot, i.e. the same cache lines, instead of 64 unrelated ones per gather instruction
+    {
+        constexpr int M = KA > W ? 2 : 1;
+        uint32_t v[M];
+        v[0] = e0 < KA ? (uint32_t)r0 : 0xFFFFFFFFu;
+        if (M > 1) v[M - 1] = e1 < KA ? (uint32_t)r1 : 0xFFFFFFFFu;
+        grp_bitonic_sort32<W, M>(v, lg.hl);
+        if (e0 < KA) alist[(int64_t)e0 * N + i] = (int32_t)v[0];
+        if (M > 1 && e1 < KA) alist[(int64_t)e1 * N + i] = (int32_t)v[M - 1];
+    }
+    // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
+    // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))
+    const unsigned long long mx = grp_max_u64<W>(m0 > m1 ? m0 : m1);
+    const float D = partial ? r_s * (1.f - 1e-6f) : sqrtf(__uint_as_float((unsigned)(mx >> 32)));
+    if (lg.hl == 0) anc[i] = make_float4(q.x, q.y, q.z, D);
+    return true;
+}
+
 // One query per lane group of W lanes (grid-stride): DENSE = every active row (radius from the cell occupancy), else
 // the rows of `list` (the anchor test's failures, radius from the old anchor).  Spilled rows go to `spill` for
 // k_knn_redo_wave.
@@ -416,76 +523,9 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
             }
             r_s = a.w * PCD_RQ_RSCALE;
         }
-        unsigned long long cap = 0;
-        int cnt = 0;
-        bool big = false, ok = false;
-        // a radius holding at most kstore points is widened (x 1.6, twice) before the query spills
-#pragma unroll 1
-        for (int attempt = 0; attempt < 3; ++attempt) {
-            if (attempt > 0) r_s *= 1.6f;
-            cap = ((unsigned long long)__float_as_uint(r_s * r_s) << 32) | 0xFFFFFFFFull;
-            const float rr = r_s * 1.0001f + 1e-30f;
-            int lo[3], hi[3];
-            cell_box(g, q, rr, lo, hi);
-            cnt = 0;
-            const int64_t nbox = (int64_t)(hi[0] - lo[0] + 1) * (hi[1] - lo[1] + 1) * (hi[2] - lo[2] + 1);
-            big = nbox > kRqMaxCells;
-            if (big) break;
-            const bool clean = rq_scan_box<KA, W>(g, q, lo, hi, cap, buf, cnt, &s_cells[gid], lg);
-            ok = clean && cnt > kstore;
-            if (ok || !clean) break;
-            wave_sync();
-        }
-#if defined(PCD_EXP_RQ) && PCD_EXP_RQ >= 1    // timing experiment: no ordering / writes (results wrong)
-        if (cnt != -7) { wave_sync(); continue; }
-#endif
-        const bool partial = cnt < KA;               // (after a buffer cut cnt == KA)
-        GrpOrder<W> o{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, &lg};
-        if (ok) {
-            (void)rq_shrink<KA, W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lg);
-            ok = cnt <= 4 * W;                        // (a set that did not shrink to 4W spills)
-        }
-        if (ok) {
-            o = grp_order32<W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lg);
-            // exact order of the stored list (first kstore + its successor) and of the anchor set boundary
-            ok = order_exact<W>(o, kstore, lg);
-            ok = ok && (cnt <= KA || (o.at(KA) >> 8) != (o.at(KA - 1) >> 8));
-        }
-        if (!ok) {
-            wave_sync();
-            if (lg.hl == 0) {
-                spill[atomicAdd(spill_cnt, 1u)] = (int32_t)i;
-                atomicAdd(big ? spill_cnt + 1 : spill_cnt + 2, 1u);   // RqStats::spill_big / spill_amb
-            }
-            continue;
-        }
-        // this lane's elements hl and W + hl of the order; unused slots of a partial set hold -1 (the anchor test
-        // gives them an infinite distance)
-        const int e0 = lg.hl, e1 = W + lg.hl;
-        const bool h0 = e0 < KA && e0 < cnt, h1 = e1 < KA && e1 < cnt;
-        const unsigned long long m0 = h0 ? buf[o.s0 & 255u] : 0ull;
-        const unsigned long long m1 = h1 ? buf[o.s1 & 255u] : 0ull;
-        const int32_t r0 = h0 ? (int32_t)(uint32_t)(m0 & 0xFFFFFFFFull) : -1;
-        const int32_t r1 = h1 ? (int32_t)(uint32_t)(m1 & 0xFFFFFFFFull) : -1;
-        if (e0 < kstore) idx[(int64_t)e0 * N + i] = r0;
-        if (e1 < kstore) idx[(int64_t)e1 * N + i] = r1;
-        // the anchor set is stored in RANK order (unused slots last): the anchor test ranks it by distance itself,
-        // and neighbouring rows -- neighbouring lanes of its waves -- then gather nearly the same snapshot rows in the
-        // same slot, i.e. the same cache lines, instead of 64 unrelated ones per gather instruction
-        {
-            constexpr int M = KA > W ? 2 : 1;
-            uint32_t v[M];
-            v[0] = e0 < KA ? (uint32_t)r0 : 0xFFFFFFFFu;
-            if (M > 1) v[M - 1] = e1 < KA ? (uint32_t)r1 : 0xFFFFFFFFu;
-            grp_bitonic_sort32<W, M>(v, lg.hl);
-            if (e0 < KA) alist[(int64_t)e0 * N + i] = (int32_t)v[0];
-            if (M > 1 && e1 < KA) alist[(int64_t)e1 * N + i] = (int32_t)v[M - 1];
-        }
-        // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
-        // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))
-        const unsigned long long mx = grp_max_u64<W>(m0 > m1 ? m0 : m1);
-        const float D = partial ? r_s * (1.f - 1e-6f) : sqrtf(__uint_as_float((unsigned)(mx >> 32)));
-        if (lg.hl == 0) anc[i] = make_float4(q.x, q.y, q.z, D);
+        const bool done = rq_query<KA, W>(g, GridSrc{&g}, i, q, r_s, N, kstore, anc, alist, idx, spill, spill_cnt, buf,
+                                          &s_cells[gid], lg);
+        (void)done;                                   // (GridSrc covers every box)
         wave_sync();                                  // buf is free for the next query
     }
 }
