@@ -65,35 +65,27 @@ static constexpr int kWinHaloNvt2 = 512;
 static constexpr int kWinHaloPhase = 128;
 template <int H> struct WinSize { static constexpr int rows = 256 + 2 * H; };
 static constexpr int kWinRows = WinSize<kWinHalo>::rows;
-#ifndef PCD_WIN_SPLIT
-#define PCD_WIN_SPLIT 0
-#endif
 template <int H = kWinHalo>
 struct WinRows {
     const float4* g;
     const float4* s;
     int64_t lo;
     PCD_DEV Vec3 operator()(int64_t j) const {
-        const uint64_t o = (uint64_t)(j - lo);
-        float4 q;
-#if PCD_WIN_SPLIT
-        // every lane reads LDS (a clamped slot), only the lanes outside the window issue a global load: the two
-        // loads cannot be merged into one flat load, which would send every lane through the texture path
-        const bool in = o < (uint64_t)WinSize<H>::rows;
-        const float4 sv = s[in ? o : 0];
-        if (in) q = sv;
-        else q = g[j];
-#else
-        if (o < (uint64_t)WinSize<H>::rows) q = s[o];
-        else q = g[j];
-#endif
+        // one 64-bit base select and one scaled add (32-bit row arithmetic: rows < 2^31): the LDS base is biased by
+        // -lo rows so that base + 16 j addresses s[j - lo] through the flat aperture.  (Measured against a ds_read for
+        // the lanes inside + a masked global load for the others: that split is slower, NVT1 1.20 -> 1.25 ms.)
+        const uint32_t j32 = (uint32_t)j;
+        const bool in = j32 - (uint32_t)lo < (uint32_t)WinSize<H>::rows;
+        const uint64_t sb = (uint64_t)(uintptr_t)s - (uint64_t)(uint32_t)lo * 16u;
+        const uint64_t base = in ? sb : (uint64_t)(uintptr_t)g;
+        const float4 q = *reinterpret_cast<const float4*>(base + (uint64_t)j32 * 16u);
         return v3(q.x, q.y, q.z);
     }
 };
 // Stage rows [lo, lo + kWinRows) of a and b (clipped to [0, N)) for the block whose first active row is i_first.
 // on == 0 (pcd_denoiser_set_windows, block-uniform): nothing is staged and every row is read from global memory --
 // the reference path the windowed reads are checked against bitwise.
-static constexpr int64_t kNoWindow = -(1ll << 60);
+static constexpr int64_t kNoWindow = -(1ll << 60) + (1ll << 31);   // (low 32 bits 2^31: no row is inside)
 template <int H = kWinHalo>
 PCD_DEV int64_t stage_window(const float4* __restrict__ a, const float4* __restrict__ b, int64_t N, int64_t i_first,
                              float4* sa, float4* sb, int on) {
@@ -353,6 +345,9 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
 // run on a side stream while the re-anchoring search works on the others (pcd_denoiser::side).
 // UNIT: the normals are the loop's own normalised f_n (every iteration after the first since load): the vote's
 // margin is a constant (nvt_tensor).
+#ifndef PCD_NVT1_WIN
+#define PCD_NVT1_WIN 1
+#endif
 #ifndef PCD_NVT1_OCC
 #define PCD_NVT1_OCC 1
 #endif
@@ -362,6 +357,7 @@ __global__ __launch_bounds__(256, PCD_NVT1_OCC) void k_nvt1(GridView g, const fl
                                                int kstore, float rho, float tau, float damp, Cover cov,
                                                float4* __restrict__ fn, int* __restrict__ err, int win,
                                                const uint8_t* __restrict__ skip) {
+#if PCD_NVT1_WIN
     __shared__ float4 s_pos[kWinRows], s_nrm[kWinRows];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
     const int64_t lo = stage_window(pos, nrm, N, rm(b0), s_pos, s_nrm, win);
@@ -370,6 +366,13 @@ __global__ __launch_bounds__(256, PCD_NVT1_OCC) void k_nvt1(GridView g, const fl
     if (skip && skip[t0]) return;
     nvt1_row<K, UNIT>(g, pos, nrm, idx, N, rm(t0), k, kstore, rho, tau, damp, cov, fn, err, WinRows<>{pos, s_pos, lo},
                 WinRows<>{nrm, s_nrm, lo});
+#else
+    (void)win;
+    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (t0 >= rm.nq) return;
+    if (skip && skip[t0]) return;
+    nvt1_row<K, UNIT>(g, pos, nrm, idx, N, rm(t0), k, kstore, rho, tau, damp, cov, fn, err, Rows4{pos}, Rows4{nrm});
+#endif
 }
 
 // The rows of list[0 .. *cnt) (the re-anchored rows, spatially sparse: no LDS window), grid-stride.

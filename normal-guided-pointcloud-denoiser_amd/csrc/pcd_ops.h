@@ -70,13 +70,21 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF n
     const float cthr = cosf(rho);
     const float cthr2 = cthr > 0.f ? cthr * cthr : -1.f;
     const bool w_self = acosf(0.f) > rho;   // the vote of a coincident neighbour (every row lists itself)
+    // Packed fp32 (v_pk_mul / v_pk_add on gfx950: two lanes of a register pair per instruction) for the pairs of
+    // products and sums; every component is the same IEEE multiply / add in the same order as the scalar code.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 vixy = {vi.x, vi.y};
+    f2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f}, acc2 = {0.f, 0.f};   // (w00, w01), (w02, w11), (w12, w22)
     auto body2 = [&](const Vec3 vj, const Vec3 nj) {
-        const Vec3 dv = vj - vi;
+        const f2 dxy = f2{vj.x, vj.y} - vixy;
+        const float dz = vj.z - vi.z;
 #if defined(PCD_EXP_NOVOTE)
-        const bool w = dv.x > 0.f;
+        const bool w = dxy.x > 0.f;
 #else
-        const float sq = sq3(dv);
-        const float e = (dv.x * nj.x + dv.y * nj.y) + dv.z * nj.z;
+        const f2 sxy = dxy * dxy;
+        const float sq = (sxy.x + sxy.y) + dz * dz;
+        const f2 exy = dxy * f2{nj.x, nj.y};
+        const float e = (exy.x + exy.y) + dz * nj.z;
         const float lhs = e * e, rhs = cthr2 * sq;
         float m;
         if constexpr (UNIT) {
@@ -91,18 +99,20 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF n
         bool w = sq == 0.f ? w_self : lhs < rhs;
         if (near) {
             const float den = fmaxf(sqrtf(sq), 1e-12f);
-            const Vec3 dn = v3(dv.x / den, dv.y / den, dv.z / den);
+            const Vec3 dn = v3(dxy.x / den, dxy.y / den, dz / den);
             float c = dot3(dn, nj);
             c = fabsf(fminf(fmaxf(c, -1.f), 1.f));
             w = acosf(c) > rho;
         }
 #endif
         const Vec3 nw = w ? nj : v3(0.f, 0.f, 0.f);
-        w00 += nw.x * nj.x; w01 += nw.x * nj.y; w02 += nw.x * nj.z;
-        w11 += nw.y * nj.y; w12 += nw.y * nj.z; w22 += nw.z * nj.z;
+        acc0 += f2{nw.x, nw.x} * f2{nj.x, nj.y};
+        acc1 += f2{nw.x, nw.y} * f2{nj.z, nj.y};
+        acc2 += f2{nw.y, nw.z} * f2{nj.z, nj.z};
         wsum += w ? 1 : 0;
     };
     for_neighbours<UNROLL, BATCH>(pos, nrm, cnt, nb, body2);
+    w00 = acc0.x; w01 = acc0.y; w02 = acc1.x; w11 = acc1.y; w12 = acc2.x; w22 = acc2.y;
     if (wsum == 0) {
         w00 = w01 = w02 = w11 = w12 = w22 = 0.f;
 #pragma unroll 1
