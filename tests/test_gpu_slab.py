@@ -105,6 +105,24 @@ def test_hip_slab_world2_matches_one_gpu(gpu, tmp_path):
 
 
 @pytest.mark.gpu
+def test_hip_slab_world4_matches_one_gpu(gpu, tmp_path):
+    """Four ranks sharing the GPU over gloo: two interior slabs exchange halos with a neighbour on either side,
+    as the interior ranks of the 8-GPU run do."""
+    import torch.multiprocessing as mp
+    pos, nrm = _cloud(gpu)
+    d = _d(pos)
+    out, cloud = str(tmp_path / "slab4.npz"), str(tmp_path / "cloud.npz")
+    np.savez(cloud, pos=pos.cpu().numpy(), n=nrm.cpu().numpy())
+    mp.spawn(_worker, args=(4, _free_port(), out, cloud, d), nprocs=4, join=True)
+    res = np.load(out)
+    assert int(res["halo"]) > 0
+    rp, rn = _fused(pos, nrm, d)
+    bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
+    np.testing.assert_allclose(res["pos"], rp, rtol=0, atol=1e-6 * bbox)
+    np.testing.assert_allclose(res["n"], rn, rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
 def test_hip_slab_world1_jacobi_is_the_fused_loop(gpu):
     """The Jacobi-across-classes mode with the global clamp through the staged engine (one position refresh per
     iteration instead of one per phase): bit-identical to the fused loop at world 1."""

@@ -109,11 +109,15 @@ def _worker(rank, world, port, out_path, halo_scale):
         dist.destroy_process_group()
 
 
-def _run_world2(tmp_path, halo_scale):
+def _run_world(tmp_path, halo_scale, world=2):
     import torch.multiprocessing as mp
-    out = str(tmp_path / f"slab_{halo_scale}.npz")
-    mp.spawn(_worker, args=(2, _free_port(), out, halo_scale), nprocs=2, join=True)
+    out = str(tmp_path / f"slab_{world}_{halo_scale}.npz")
+    mp.spawn(_worker, args=(world, _free_port(), out, halo_scale), nprocs=world, join=True)
     return np.load(out)
+
+
+def _run_world2(tmp_path, halo_scale):
+    return _run_world(tmp_path, halo_scale, 2)
 
 
 def test_slab_world2_gloo_matches_oracle(tmp_path):
@@ -131,3 +135,16 @@ def test_slab_world2_gloo_matches_oracle(tmp_path):
 def test_slab_world2_thin_halo_is_reported(tmp_path):
     res = _run_world2(tmp_path, 1e-4)
     assert int(res["err"]) == 2          # both ranks hold a slab face the k-balls cross
+
+
+def test_slab_world4_gloo_matches_oracle(tmp_path):
+    """Four ranks: the two interior slabs exchange halos with a neighbour on either side (the 8-GPU layout's
+    interior case), and both all-reduces span every rank."""
+    res = _run_world(tmp_path, 1.0, 4)
+    assert int(res["err"]) == 0 and int(res["halo"]) > 0
+    pos, nrm = _cloud()
+    _, d = _params(pos)
+    rp, rn = _reference(pos, nrm, d)
+    bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
+    np.testing.assert_allclose(res["pos"], rp, rtol=0, atol=1e-6 * bbox)
+    np.testing.assert_allclose(res["n"], rn, rtol=0, atol=1e-5)
