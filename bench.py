@@ -220,7 +220,7 @@ def main():
         params = nat.make_params(k=args.k, k_update=args.k_update, d=d)
         step = lambda: sd.iterate(params, 1)  # noqa: E731
     else:
-        pos, nrm, diag = make_cloud(args.points, 2 + rank, dev)
+        pos, nrm, diag, surf = make_cloud(args.points, 2 + rank, dev, clean=True)
         pc = Pointcloud(pos, nrm)
         proc = Processor(pc, k_hint=args.k)
         d = 2 * float(proc.meanEdgeLength())
@@ -291,6 +291,20 @@ def main():
         torch.cuda.synchronize()
         ten_ms = (time.perf_counter() - t10) * 1e3
         fused.check()
+    chamfer = None
+    if mode != "slab" and args.ten:
+        # the Chamfer distance of the 10-iteration result to the clean surface samples, at full size on the GPU
+        # (pcd_nn_dist: two nearest-neighbour passes over Morton-ordered queries), timed outside every bench region
+        from Pointcloud.Modules.Utils import TorchUtils
+        den = torch.empty_like(surf)
+        fused.store(den, torch.empty_like(surf))
+        torch.cuda.synchronize()
+        tc = time.perf_counter()
+        cd_den = float(TorchUtils.ChamferDistance(surf, den).mean())
+        torch.cuda.synchronize()
+        cd_ms = (time.perf_counter() - tc) * 1e3
+        cd_in = float(TorchUtils.ChamferDistance(surf, pos).mean())
+        chamfer = {"points": args.points, "ms": round(cd_ms, 3), "cd_noisy": cd_in, "cd_10_iterations": cd_den}
 
     k1_points = sd.owned_global.numel() if mode == "slab" else args.points
     k1_bytes = b_alg_knn_nvt1(args.k) * k1_points
@@ -332,6 +346,7 @@ def main():
         "iterations_per_sec": round(1e3 / ms_per_step, 2),
         "first_iteration_ms": round(first_ms, 3) if first_ms is not None else None,
         "ten_iteration_ms": round(ten_ms, 3) if ten_ms is not None else None,
+        "chamfer": chamfer,
         "kernel_ms": kernel_ms,
         "stage_bound": STAGE_BOUND if mode != "slab" else None,
         "iteration_roofline": {"bound": "hbm", "alg_bytes_per_point": b_alg_iteration(args.k, args.k_update),

@@ -248,6 +248,9 @@ PCD_DEV bool anchor_holds(float d2k, Vec3 q, float4 a) {
 // (an exact d² tie included, which the rank would break) sends the row to the redo search instead.  The
 // certificate counts candidates below the squared anchor bound, a rounding-safe restatement of anchor_holds.
 // Rows that fail take the exact redo path, so the stored lists are bit-identical to the 64-bit-key ordering.
+#ifndef PCD_ANCHOR_SORT
+#define PCD_ANCHOR_SORT oddeven_sort
+#endif
 static constexpr int kAnchorBS = 128;
 template <int K, int KA>
 __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const float4* __restrict__ pos, int64_t N,
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
                 // only unused slots (infinite distance) reach it
                 c[t] = ((uint32_t)fminf(d2 * S, 67108860.f) << 6) | (uint32_t)t;
             }
-            bitonic_sort<KA>(c);
+            PCD_ANCHOR_SORT<KA>(c);
             bool ok = below >= kstore;
 #pragma unroll
             for (int t = 0; t < K; ++t)

@@ -245,6 +245,26 @@ PCD_DEV void cswap(uint32_t& a, uint32_t& b) {
     a = lo;
 }
 
+// Ascending sort of v[0..N) by Batcher's odd-even merge network (N a power of two): 543 compare-exchanges at N = 64
+// against the bitonic network's 672, every one of them between compile-time slots; as with any sorting network the
+// compiler drops the exchanges whose outputs are never read (the anchor test reads the first kstore + 1).
+template <int N, typename T>
+PCD_DEV void oddeven_sort(T (&v)[N]) {
+#pragma unroll
+    for (int p = 1; p < N; p <<= 1) {
+#pragma unroll
+        for (int k = p; k >= 1; k >>= 1) {
+#pragma unroll
+            for (int j = k % p; j + k < N; j += 2 * k) {
+#pragma unroll
+                for (int i = 0; i < k; ++i) {
+                    if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cswap(v[i + j], v[i + j + k]);
+                }
+            }
+        }
+    }
+}
+
 // Ascending bitonic sort of v[0..N).
 template <int N, typename T>
 PCD_DEV void bitonic_sort(T (&v)[N]) {
