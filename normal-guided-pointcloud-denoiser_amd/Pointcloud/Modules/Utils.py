@@ -38,8 +38,11 @@ class SlicedTorchData:
 
 
 def _nn(ref: torch.Tensor, q: torch.Tensor):
-    """For every row of q: (squared distance, index) of its nearest row of ref (pcd_nn_dist)."""
-    grid = _nat.Grid(ref, k_hint=1)
+    """For every row of q: (squared distance, index) of its nearest row of ref (pcd_nn_dist).  The grid is sized for
+    ~16 points a cell: the queries of an error metric (a noisy or denoised cloud against its surface) sit several point
+    spacings off ref, and coarser cells reach them in fewer probes (10M points: 42 ms against 276 ms with ~1 point a
+    cell, tools/nn_probe.py); the result is exact either way."""
+    grid = _nat.Grid(ref, k_hint=32)
     return grid.nn(q)
 
 

@@ -713,7 +713,10 @@ struct pcd_denoiser {
     RowMap rowmap() const { return RowMap{rows, rows ? n_rows : n}; }
 };
 
-static const int kNumPart = 1024;
+#ifndef PCD_NUM_PART
+#define PCD_NUM_PART 1024
+#endif
+static const int kNumPart = PCD_NUM_PART;   // blocks of the flat reductions (grid-stride), = their partials
 // Timing events per iteration: start, after the anchor test (+ redo-list select), after the re-anchoring search,
 // after the exact-key spill search, after NVT1 (= end of K1), after NVT2, after each of 3 phases, after finish, end.
 static const int kTimingSets = 256, kTimingEvents = 11;

@@ -172,6 +172,95 @@ PCD_DEV bool search_done(const GridView& g, Vec3 q, int cx, int cy, int cz, int 
     return exhausted || kth <= bound * bound * 0.99998f;
 }
 
+// Is the top-k final once every cell of the box [lo, hi] (cell coordinates) is scanned?  (The box's faces that are
+// not at the grid's edge bound the distance to every unscanned cell.)
+PCD_DEV bool box_done(const GridView& g, Vec3 q, const int lo[3], const int hi[3], float kth) {
+    bool exhausted = true;
+    float bound = 3.0e38f;
+    const int dm[3] = {g.dx, g.dy, g.dz};
+    const float o[3] = {g.ox, g.oy, g.oz};
+    const float qa[3] = {q.x, q.y, q.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (lo[a] > 0) {
+            exhausted = false;
+            bound = fminf(bound, fmaxf(qa[a] - (o[a] + lo[a] * g.h), 0.f));
+        }
+        if (hi[a] < dm[a] - 1) {
+            exhausted = false;
+            bound = fminf(bound, fmaxf((o[a] + (hi[a] + 1) * g.h) - qa[a], 0.f));
+        }
+    }
+    return exhausted || kth <= bound * bound * 0.99998f;
+}
+
+// Brick shells (4x4x4 cells) around the query's brick, after the cells within Chebyshev radius RC of (cx, cy, cz)
+// have been scanned: one hash probe per brick instead of one per cell, so a query many cells away from the cloud
+// (noisy points off a finely gridded surface) pays ~64x fewer probes.  Cells inside the scanned block are skipped.
+static constexpr int kCellShells = 3;
+template <int K, bool ORIG>
+PCD_DEV void brick_shells(const GridView& g, Vec3 q, int cx, int cy, int cz, TopK<K>& tk, unsigned long long cap) {
+    const int RC = kCellShells;
+    const int bx = cx >> 2, by = cy >> 2, bz = cz >> 2;
+    const int nbx = (g.dx + 3) >> 2, nby = (g.dy + 3) >> 2, nbz = (g.dz + 3) >> 2;
+#pragma unroll 1
+    for (int Rb = 0;; ++Rb) {
+        const int64_t side = 2 * (int64_t)Rb + 1;
+        if (Rb > 8 && side * side * side > (int64_t)g.n / 4) {   // a far outlier: one exhaustive scan is cheaper
+            tk.init(cap);
+            scan_range<K, ORIG>(g.pts, 0, (uint32_t)g.n, q, tk);
+            return;
+        }
+#pragma unroll 1
+        for (int dz = -Rb; dz <= Rb; ++dz) {
+#pragma unroll 1
+            for (int dy = -Rb; dy <= Rb; ++dy) {
+                const bool rim = (dz == -Rb || dz == Rb || dy == -Rb || dy == Rb);
+                const int step = rim ? 1 : 2 * Rb;
+#pragma unroll 1
+                for (int dx = -Rb; dx <= Rb; dx += (step > 0 ? step : 1)) {
+                    const int qx = bx + dx, qy = by + dy, qz = bz + dz;
+                    if ((unsigned)qx >= (unsigned)nbx || (unsigned)qy >= (unsigned)nby || (unsigned)qz >= (unsigned)nbz)
+                        continue;
+                    const float lx = g.ox + 4 * qx * g.h, ly = g.oy + 4 * qy * g.h, lz = g.oz + 4 * qz * g.h;
+                    const float gx = axis_gap(q.x, lx, lx + 4 * g.h), gy = axis_gap(q.y, ly, ly + 4 * g.h),
+                                gz = axis_gap(q.z, lz, lz + 4 * g.h);
+                    if (gx * gx + gy * gy + gz * gz > tk.kth() * 1.00001f + 1e-30f) continue;
+                    const unsigned long long bkey = morton3(qx, qy, qz);
+                    unsigned long long slot = hash_slot(bkey, g.hbits);
+                    uint32_t brick = ~0u;
+                    for (;;) {
+                        const uint4 sl = *reinterpret_cast<const uint4*>(g.table + slot);
+                        const unsigned long long k2 = (unsigned long long)sl.x | ((unsigned long long)sl.y << 32);
+                        if (k2 == bkey) { brick = sl.z; break; }
+                        if (k2 == kEmptyKey) break;
+                        slot = (slot + 1) & g.mask;
+                    }
+                    if (brick == ~0u) continue;
+#pragma unroll 1
+                    for (int loc = 0; loc < 64; ++loc) {
+                        // local cell (x, y, z) of Morton slot loc: bits 0/3 -> x, 1/4 -> y, 2/5 -> z
+                        const int ccx = 4 * qx + ((loc & 1) | ((loc >> 2) & 2));
+                        const int ccy = 4 * qy + (((loc >> 1) & 1) | ((loc >> 3) & 2));
+                        const int ccz = 4 * qz + (((loc >> 2) & 1) | ((loc >> 4) & 2));
+                        if (abs(ccx - cx) <= RC && abs(ccy - cy) <= RC && abs(ccz - cz) <= RC) continue;   // scanned
+                        const float ex = g.ox + ccx * g.h, ey = g.oy + ccy * g.h, ez = g.oz + ccz * g.h;
+                        const float hx = axis_gap(q.x, ex, ex + g.h), hy = axis_gap(q.y, ey, ey + g.h),
+                                    hz = axis_gap(q.z, ez, ez + g.h);
+                        if (hx * hx + hy * hy + hz * hz > tk.kth() * 1.00001f + 1e-30f) continue;
+                        const uint2 c = g.cells[(uint64_t)brick * 64 + loc];
+                        if (c.y > c.x) scan_range<K, ORIG>(g.pts, c.x, c.y, q, tk);
+                    }
+                }
+            }
+        }
+        // scanned: the bricks within Rb (and the cell block within RC, inside them from Rb >= 1 on)
+        const int lo[3] = {4 * (bx - Rb), 4 * (by - Rb), 4 * (bz - Rb)};
+        const int hi[3] = {4 * (bx + Rb) + 3, 4 * (by + Rb) + 3, 4 * (bz + Rb) + 3};
+        if (Rb >= 1 && box_done(g, q, lo, hi, tk.kth())) return;
+    }
+}
+
 // Exact top-K of the snapshot for query q (entries beyond the seed's rank are only valid when cap == inf).
 template <int K, bool ORIG>
 PCD_DEV void knn_search(const GridView& g, Vec3 q, TopK<K>& tk, unsigned long long cap = kInfKey) {
@@ -187,12 +276,8 @@ PCD_DEV void knn_search(const GridView& g, Vec3 q, TopK<K>& tk, unsigned long lo
     while (!search_done(g, q, cx, cy, cz, R, tk.kth())) {
         ++R;
         PCD_KSTAT(tk, 5, 1);
-        // A far outlier keeps growing Chebyshev shells (an empty cell costs one hash probe) until the block would
-        // hold more cells than the cloud has points -- only then is one exhaustive scan cheaper.
-        const int64_t side = 2 * (int64_t)R + 1;
-        if (R > 24 && side * side * side > (int64_t)g.n) {
-            tk.init(cap);
-            scan_range<K, ORIG>(g.pts, 0, (uint32_t)g.n, q, tk);
+        if (R > kCellShells) {        // still open after the cell shells: continue brick by brick
+            brick_shells<K, ORIG>(g, q, cx, cy, cz, tk, cap);
             return;
         }
 #pragma unroll 1
