@@ -168,6 +168,7 @@ typedef struct {
                             (PostProcessing.ipynb:1088-1089, mask = ||temp_pos - original_pos|| < d); 0: off */
 } pcd_denoise_params;
 
+/* g: the frozen snapshot, at most 2^28 points (268M; larger clouds run as spatial slabs, pcd_slab). */
 int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out);
 int pcd_denoiser_destroy(pcd_denoiser* dn);
 /* pos, n: caller rows [N][3] (original order, N = grid n) -> internal spatial order */

@@ -29,16 +29,28 @@
 namespace pcd {
 int knn_cap(int k);
 
+// Element i of a column whose base is uniform: a 32-bit byte offset (i * sizeof(T) < 4 GiB, checked on the host:
+// N < 2^28 for the anchored path) lets the load take the base in SGPRs and one offset VGPR (global_load ... saddr),
+// where 64-bit per-lane addresses cost a multiply-add and moves per column.
+template <class T>
+PCD_DEV const T* at32(const T* base, int64_t i) {
+    return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (uint32_t)((uint32_t)i * (uint32_t)sizeof(T)));
+}
+template <class T>
+PCD_DEV T* at32(T* base, int64_t i) {
+    return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (uint32_t)((uint32_t)i * (uint32_t)sizeof(T)));
+}
+
 struct ColNb {
     const int32_t* idx;
     int64_t n, i;
-    PCD_DEV int64_t operator()(int t) const { return idx[(int64_t)t * n + i]; }
+    PCD_DEV int64_t operator()(int t) const { return *at32(idx + (int64_t)t * n, i); }
 };
 // Same, for a list read exactly once (NVT2): streamed past L2 so the neighbour gathers keep it.
 struct ColNbStream {
     const int32_t* idx;
     int64_t n, i;
-    PCD_DEV int64_t operator()(int t) const { return __builtin_nontemporal_load(idx + (int64_t)t * n + i); }
+    PCD_DEV int64_t operator()(int t) const { return __builtin_nontemporal_load(at32(idx + (int64_t)t * n, i)); }
 };
 // A column-major list re-read from memory with out-of-range entries mapped to the row itself (the fallback pass
 // of nvt_tensor; an invalid entry is already reported by the kernel's own check).
@@ -46,7 +58,7 @@ struct ColNbSafe {
     const int32_t* idx;
     int64_t n, i;
     PCD_DEV int64_t operator()(int t) const {
-        const int64_t j = idx[(int64_t)t * n + i];
+        const int64_t j = *at32(idx + (int64_t)t * n, i);
         return (uint64_t)j < (uint64_t)n ? j : i;
     }
 };
@@ -279,14 +291,14 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
             const float S = 67108864.f / fmaxf(R * R, 1e-30f);
             uint32_t r[KA], c[KA];
 #pragma unroll
-            for (int t = 0; t < KA; ++t) r[t] = (uint32_t)__builtin_nontemporal_load(alist + (int64_t)t * N + i);
+            for (int t = 0; t < KA; ++t) r[t] = (uint32_t)__builtin_nontemporal_load(at32(alist + (int64_t)t * N, i));
             int below = 0;
 #pragma unroll
             for (int t = 0; t < KA; ++t) {
                 const bool slot = r[t] < (uint32_t)N;   // -1: unused slot of a partial anchor set
                 const uint32_t rt = slot ? r[t] : 0u;
                 s_r[t * kAnchorBS + threadIdx.x] = rt;
-                const float d2r = dist2(vi, g.pts[rt]);   // unconditional load: all KA gathers stay in flight
+                const float d2r = dist2(vi, *at32(g.pts, rt));   // unconditional load: all KA gathers in flight
                 const float d2 = slot ? d2r : __int_as_float(0x7F800000);
                 below += d2 < T ? 1 : 0;
                 // clamp below 2^26 in fp32 (2^26 - 1 rounds UP to 2^26, which would wrap to 0 after the shift);
@@ -304,7 +316,7 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
                 for (int t = 0; t < K; ++t)
                     if (t < kstore)
                         __builtin_nontemporal_store((int32_t)s_r[(c[t] & 63u) * kAnchorBS + threadIdx.x],
-                                                    idx + (int64_t)t * N + i);
+                                                    at32(idx + (int64_t)t * N, i));
             }
         }
     }
@@ -324,7 +336,7 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
     bool bad = false;
 #pragma unroll
     for (int t = 0; t < K; ++t) {
-        l[t] = t < kstore ? idx[(int64_t)t * N + i] : (int)i;
+        l[t] = t < kstore ? *at32(idx + (int64_t)t * N, i) : (int)i;
         if ((uint32_t)l[t] >= (uint32_t)N) { bad = true; l[t] = (int)i; }
     }
     if (bad) atomicOr(err, 1);
@@ -1008,6 +1020,8 @@ int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out) {
     *out = nullptr;
     PCD_CHECK_ARG(g != nullptr, "grid is null");
     PCD_CHECK_ARG(k_max >= 1 && k_max <= pcd_max_k(), "k_max out of range");
+    // the kernels address rows and list columns by 32-bit byte offsets from uniform bases (at32): 16 B x N < 4 GiB
+    PCD_CHECK_ARG(g->n < (1ll << 28), "more than 2^28 points per denoiser (split into spatial slabs)");
     pcd_denoiser* dn = new pcd_denoiser();
     dn->g = g;
     dn->n = g->n;
