@@ -165,8 +165,8 @@ def measured_traffic(points, k, ms_per_step):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--points", type=int, default=10_000_000)
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--k-update", type=int, default=8)
