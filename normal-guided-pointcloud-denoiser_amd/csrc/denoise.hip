@@ -72,7 +72,10 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 // measured limiter of the NVT kernels (TA busy 65-77 %); LDS serves them in a few.
 // Rows staged on either side of the block's own rows, per kernel (A/B'd at 10M with tools/ab_bench.sh: NVT2 gains
 // 0.16 ms from 512, the flat phase loses 0.06 ms from it and gains 0.01 ms from 128).
-static constexpr int kWinHalo = 256;                    // NVT1
+#ifndef PCD_NVT1_HALO
+#define PCD_NVT1_HALO 256
+#endif
+static constexpr int kWinHalo = PCD_NVT1_HALO;          // NVT1
 static constexpr int kWinHaloNvt2 = 512;
 static constexpr int kWinHaloPhase = 128;
 template <int H> struct WinSize { static constexpr int rows = 256 + 2 * H; };
@@ -295,14 +298,14 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
             int below = 0;
 #pragma unroll
             for (int t = 0; t < KA; ++t) {
-                const bool slot = r[t] < (uint32_t)N;   // -1: unused slot of a partial anchor set
-                const uint32_t rt = slot ? r[t] : 0u;
+                // an unused slot of a partial anchor set holds N: the snapshot's +inf sentinel row (the min keeps any
+                // entry inside the allocation)
+                const uint32_t rt = min(r[t], (uint32_t)N);
                 s_r[t * kAnchorBS + threadIdx.x] = rt;
-                const float d2r = dist2(vi, *at32(g.pts, rt));   // unconditional load: all KA gathers in flight
-                const float d2 = slot ? d2r : __int_as_float(0x7F800000);
+                const float d2 = dist2(vi, *at32(g.pts, rt));   // unconditional load: all KA gathers in flight
                 below += d2 < T ? 1 : 0;
                 // clamp below 2^26 in fp32 (2^26 - 1 rounds UP to 2^26, which would wrap to 0 after the shift);
-                // only unused slots (infinite distance) reach it
+                // only the sentinel's infinite distance reaches it
                 c[t] = ((uint32_t)fminf(d2 * S, 67108860.f) << 6) | (uint32_t)t;
             }
             PCD_ANCHOR_SORT<KA>(c);
@@ -434,7 +437,7 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
             const float4 a = anc[i];
             // (D + |q - a|)² bounds the KA-th key at q only for a FULL anchor set (KA points within D of a); a partial
             // set (fewer points within its radius, unused slots -1) gives no such bound
-            if (a.w >= 0.f && alist[(int64_t)(KA - 1) * N + i] >= 0) cap = anchor_cap(q, a);
+            if (a.w >= 0.f && (uint32_t)alist[(int64_t)(KA - 1) * N + i] < (uint32_t)N) cap = anchor_cap(q, a);
         }
         const unsigned long long top = wave_knn<KA>(g, q, cap, s_buf[wv], &s_cells[wv], lane);
         // a slot without a finite candidate (non-finite query, fewer than KA points) is never stored as an index:

@@ -80,6 +80,12 @@ __global__ void k_gather_sorted(const float* __restrict__ xyz, const int32_t* __
     pts[r] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], __uint_as_float((uint32_t)i));
 }
 
+// pts[n]: a row at +inf, the stand-in for the unused slots of a partial anchor set (rank n): its distance to any
+// finite query is +inf, so the anchor test needs no per-slot validity select
+__global__ void k_sentinel(float4* __restrict__ p) {
+    if (threadIdx.x == 0) *p = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+}
+
 // number of distinct (key >> shift) values of a sorted key array
 __global__ void k_count_starts(const unsigned long long* __restrict__ keys, int64_t n, int shift, unsigned long long* count) {
     const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -387,7 +393,7 @@ int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, const fl
     auto free_tmp = [&]() { (void)hipFree(keys); (void)hipFree(keys2); (void)hipFree(vals); (void)hipFree(tmp); (void)hipFree(cnt); };
     if (hipMalloc(&keys, n * 8) != hipSuccess || hipMalloc(&keys2, n * 8) != hipSuccess ||
         hipMalloc(&vals, n * 4) != hipSuccess || hipMalloc(&g->perm, n * 4) != hipSuccess ||
-        hipMalloc(&g->pts, n * sizeof(float4)) != hipSuccess || hipMalloc(&cnt, 16) != hipSuccess) {
+        hipMalloc(&g->pts, (n + 1) * sizeof(float4)) != hipSuccess || hipMalloc(&cnt, 16) != hipSuccess) {
         free_tmp(); cleanup(); return fail(PCD_ERR_OOM, "pcd_grid_build: device allocation");
     }
     const dim3 blk(256), grd((unsigned)cdiv(n, 256));
@@ -398,6 +404,7 @@ int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, const fl
         free_tmp(); cleanup(); return fail(PCD_ERR_HIP, "rocprim::radix_sort_pairs failed");
     }
     hipLaunchKernelGGL(k_gather_sorted, grd, blk, 0, st, xyz, g->perm, n, g->pts);
+    hipLaunchKernelGGL(k_sentinel, dim3(1), dim3(64), 0, st, g->pts + n);
     (void)hipMemsetAsync(cnt, 0, 16, st);
     hipLaunchKernelGGL(k_count_starts, grd, blk, 0, st, keys2, n, 0, cnt);
     hipLaunchKernelGGL(k_count_starts, grd, blk, 0, st, keys2, n, 6, cnt + 1);

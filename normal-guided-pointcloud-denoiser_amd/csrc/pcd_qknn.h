@@ -448,8 +448,8 @@ PCD_DEV bool rq_query(const GridView& g, const Src& src, int64_t i, Vec3 q, floa
     const bool h0 = e0 < KA && e0 < cnt, h1 = e1 < KA && e1 < cnt;
     const unsigned long long m0 = h0 ? buf[o.s0 & 255u] : 0ull;
     const unsigned long long m1 = h1 ? buf[o.s1 & 255u] : 0ull;
-    const int32_t r0 = h0 ? (int32_t)(uint32_t)(m0 & 0xFFFFFFFFull) : -1;
-    const int32_t r1 = h1 ? (int32_t)(uint32_t)(m1 & 0xFFFFFFFFull) : -1;
+    const int32_t r0 = h0 ? (int32_t)(uint32_t)(m0 & 0xFFFFFFFFull) : (int32_t)N;   // N: the +inf sentinel row
+    const int32_t r1 = h1 ? (int32_t)(uint32_t)(m1 & 0xFFFFFFFFull) : (int32_t)N;
     if (e0 < kstore) idx[(int64_t)e0 * N + i] = r0;
     if (e1 < kstore) idx[(int64_t)e1 * N + i] = r1;
     // the anchor set is stored in RANK order (unused slots last): the anchor test ranks it by distance itself,
