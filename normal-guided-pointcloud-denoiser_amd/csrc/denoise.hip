@@ -78,9 +78,13 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 static constexpr int kWinHalo = PCD_NVT1_HALO;          // NVT1
 static constexpr int kWinHaloNvt2 = 512;
 static constexpr int kWinHaloPhase = 128;
-template <int H> struct WinSize { static constexpr int rows = 256 + 2 * H; };
-static constexpr int kWinRows = WinSize<kWinHalo>::rows;
-template <int H = kWinHalo>
+template <int H, int BS = 256> struct WinSize { static constexpr int rows = BS + 2 * H; };
+#ifndef PCD_NVT_BS
+#define PCD_NVT_BS 256
+#endif
+static constexpr int kNvtBS = PCD_NVT_BS;   // threads per NVT block (512 measured: fewer blocks fit the LDS, NVT2 0.92 -> 1.23 ms)
+static constexpr int kWinRows = WinSize<kWinHalo, kNvtBS>::rows;
+template <int H = kWinHalo, int BS = kNvtBS>
 struct WinRows {
     const float4* g;
     const float4* s;
@@ -90,7 +94,7 @@ struct WinRows {
         // -lo rows so that base + 16 j addresses s[j - lo] through the flat aperture.  (Measured against a ds_read for
         // the lanes inside + a masked global load for the others: that split is slower, NVT1 1.20 -> 1.25 ms.)
         const uint32_t j32 = (uint32_t)j;
-        const bool in = j32 - (uint32_t)lo < (uint32_t)WinSize<H>::rows;
+        const bool in = j32 - (uint32_t)lo < (uint32_t)WinSize<H, BS>::rows;
         const uint64_t sb = (uint64_t)(uintptr_t)s - (uint64_t)(uint32_t)lo * 16u;
         const uint64_t base = in ? sb : (uint64_t)(uintptr_t)g;
         const float4 q = *reinterpret_cast<const float4*>(base + (uint64_t)j32 * 16u);
@@ -101,13 +105,13 @@ struct WinRows {
 // on == 0 (pcd_denoiser_set_windows, block-uniform): nothing is staged and every row is read from global memory --
 // the reference path the windowed reads are checked against bitwise.
 static constexpr int64_t kNoWindow = -(1ll << 60) + (1ll << 31);   // (low 32 bits 2^31: no row is inside)
-template <int H = kWinHalo>
+template <int H = kWinHalo, int BS = kNvtBS>
 PCD_DEV int64_t stage_window(const float4* __restrict__ a, const float4* __restrict__ b, int64_t N, int64_t i_first,
                              float4* sa, float4* sb, int on) {
     if (!on) return kNoWindow;
     int64_t lo = i_first - H;
     lo = lo < 0 ? 0 : lo;
-    for (int r = threadIdx.x; r < WinSize<H>::rows; r += blockDim.x) {
+    for (int r = threadIdx.x; r < WinSize<H, BS>::rows; r += blockDim.x) {
         const int64_t j = lo + r;
         if (j < N) { sa[r] = a[j]; sb[r] = b[j]; }
     }
@@ -370,7 +374,7 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
 #define PCD_NVT1_OCC 1
 #endif
 template <int K, bool UNIT>
-__global__ __launch_bounds__(256, PCD_NVT1_OCC) void k_nvt1(GridView g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
+__global__ __launch_bounds__(kNvtBS, PCD_NVT1_OCC) void k_nvt1(GridView g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                int kstore, float rho, float tau, float damp, Cover cov,
                                                float4* __restrict__ fn, int* __restrict__ err, int win,
@@ -464,20 +468,20 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
 #define PCD_NVT2_NORM false
 #endif
 template <int K>
-__global__ __launch_bounds__(256) void k_nvt2(const float4* __restrict__ pos, const float4* __restrict__ fn,
+__global__ __launch_bounds__(kNvtBS) void k_nvt2(const float4* __restrict__ pos, const float4* __restrict__ fn,
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                float rho, float scale, uint8_t* __restrict__ cls,
                                                float4* __restrict__ edge, int win) {
-    __shared__ float4 s_pos[WinSize<kWinHaloNvt2>::rows], s_fn[WinSize<kWinHaloNvt2>::rows];
+    __shared__ float4 s_pos[WinSize<kWinHaloNvt2, kNvtBS>::rows], s_fn[WinSize<kWinHaloNvt2, kNvtBS>::rows];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
-    const int64_t lo = stage_window<kWinHaloNvt2>(pos, fn, N, rm(b0), s_pos, s_fn, win);
+    const int64_t lo = stage_window<kWinHaloNvt2, kNvtBS>(pos, fn, N, rm(b0), s_pos, s_fn, win);
     const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 p4 = pos[i];
     // classes and the edge vector are invariant to the positive scale 1/Σw (ratios of eigenvalues, a unit
     // eigenvector): the tensor is left unnormalised.  f_n is NVT1's normalised output: the vote margin is constant.
-    const Sym3 T = nvt_tensor<K, PCD_NVT2_NORM, true>(WinRows<kWinHaloNvt2>{pos, s_pos, lo}, WinRows<kWinHaloNvt2>{fn, s_fn, lo},
+    const Sym3 T = nvt_tensor<K, PCD_NVT2_NORM, true>(WinRows<kWinHaloNvt2, kNvtBS>{pos, s_pos, lo}, WinRows<kWinHaloNvt2, kNvtBS>{fn, s_fn, lo},
                                                 v3(p4.x, p4.y, p4.z), k, ColNbStream{idx, N, i}, rho, ColNbSafe{idx, N, i});
 #ifdef PCD_NVT2_LAPACK
     float w[3], V[3][3];
@@ -627,10 +631,10 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
                                                 const float4* __restrict__ orig, float clampg) {
     // the flat phase moves most rows: its neighbour rows come from an LDS window of pin / fn around the block
     constexpr bool WIN = PCD_PHASE_WIN && (KIND == PCD_STEP_FLAT);
-    __shared__ float4 s_pos[WIN ? WinSize<kWinHaloPhase>::rows : 1], s_fn[WIN ? WinSize<kWinHaloPhase>::rows : 1];
+    __shared__ float4 s_pos[WIN ? WinSize<kWinHaloPhase, 256>::rows : 1], s_fn[WIN ? WinSize<kWinHaloPhase, 256>::rows : 1];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
     int64_t lo = 0;
-    if constexpr (WIN) lo = stage_window<kWinHaloPhase>(pin, fn, N, rm(b0 < rm.nq ? b0 : rm.nq - 1), s_pos, s_fn, win);
+    if constexpr (WIN) lo = stage_window<kWinHaloPhase, 256>(pin, fn, N, rm(b0 < rm.nq ? b0 : rm.nq - 1), s_pos, s_fn, win);
     const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
@@ -644,7 +648,7 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     const ColNb nb{idx, N, i};
     Vec3 o;
     if constexpr (WIN)
-        o = step_flat<KU>(WinRows<kWinHaloPhase>{pin, s_pos, lo}, WinRows<kWinHaloPhase>{fn, s_fn, lo}, vi, F(i), ku, nb,
+        o = step_flat<KU>(WinRows<kWinHaloPhase, 256>{pin, s_pos, lo}, WinRows<kWinHaloPhase, 256>{fn, s_fn, lo}, vi, F(i), ku, nb,
                           __uint_as_float(((const unsigned*)g)[3]), d, alpha);
     else if (KIND == PCD_STEP_FLAT) o = step_flat<KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
     else if (KIND == PCD_STEP_EDGE) o = step_edge<KU, 4>(P, F, vi, Rows4{edge}(i), ku, nb, d, alpha);
@@ -831,6 +835,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
         PCD_HIP(hipEventCreateWithFlags(&dn->join, hipEventDisableTiming));
     }
     const dim3 grd_list((unsigned)std::min<int64_t>(cdiv(rm.nq, 256), 1024));
+    const dim3 blk_nvt(kNvtBS), grd_nvt((unsigned)cdiv(rm.nq, kNvtBS));
 #define PCD_K1A(C)                                                                                                     \
     case C:                                                                                                            \
         if (dense) {                                                                                                   \
@@ -844,7 +849,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
             if (overlap) {                                                                                             \
                 PCD_HIP(hipEventRecord(dn->fork, st));                                                                 \
                 PCD_HIP(hipStreamWaitEvent(dn->side, dn->fork, 0));                                                    \
-                hipLaunchKernelGGL((k_nvt1<C, false>), grd, blk, 0, dn->side, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,   \
+                hipLaunchKernelGGL((k_nvt1<C, false>), grd_nvt, blk_nvt, 0, dn->side, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,   \
                                    p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, dn->fail);          \
                 PCD_HIP(hipEventRecord(dn->join, dn->side));                                                           \
             }                                                                                                          \
@@ -861,10 +866,10 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
                                p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->redo, redo_cnt);                 \
             PCD_HIP(hipStreamWaitEvent(st, dn->join, 0));                                                              \
         } else if (dn->unit_nrm) {                                                                                     \
-            hipLaunchKernelGGL((k_nvt1<C, true>), grd, blk, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,       \
+            hipLaunchKernelGGL((k_nvt1<C, true>), grd_nvt, blk_nvt, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,       \
                                p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, nullptr);               \
         } else {                                                                                                       \
-            hipLaunchKernelGGL((k_nvt1<C, false>), grd, blk, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,      \
+            hipLaunchKernelGGL((k_nvt1<C, false>), grd_nvt, blk_nvt, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,      \
                                p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, nullptr);               \
         }                                                                                                              \
         break;
@@ -910,7 +915,7 @@ static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t s
 static int stage_k2(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t st) {
     const RowMap rm = dn->rowmap();
     if (rm.nq == 0) return PCD_OK;
-    const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
+    const dim3 blk(kNvtBS), grd((unsigned)cdiv(rm.nq, kNvtBS));
     float4* P = dn->pos[dn->cur];
 #define PCD_K2(C) \
     case C:                                                                                                            \
