@@ -622,8 +622,8 @@ PCD_DEV Vec3 vu_smooth(const float w[3], const float V[3][3], Vec3 n, float tau,
 // NVT2's outputs are the classes (eigenvalues only) and the edge vector (the smallest eigenvalue's eigenvector,
 // used only through y·yᵀ and (x·y)·y in edge_step, Denoiser.py:53-88 -- sign-invariant).  Unlike NVT1's VU smoothing
 // (Eᵀ·M·E, Decompositionor.py:101-105), nothing here depends on LAPACK's eigenvector signs or degenerate bases, so
-// a cyclic Jacobi solve replaces the ssytd2 + ssteqr port: 4 fixed sweeps of the 3 plane rotations (fp32 Jacobi
-// converges quadratically; after 4 sweeps the off-diagonal is at rounding level), no data-dependent loop, no
+// a cyclic Jacobi solve replaces the ssytd2 + ssteqr port: 3 fixed sweeps of the 3 plane rotations (fp32 Jacobi
+// converges quadratically; after 3 sweeps the off-diagonal is at rounding level), no data-dependent loop, no
 // divergence.  Eigenvalue error ~1e-7 of the trace (the tests' bound for eigenvalues is 2e-6).
 // On the device the rotation is built from the hardware reciprocal / square-root estimates (~1 ulp): any (c, s)
 // with c² + s² = 1 to rounding keeps the similarity orthogonal, and the off-diagonal still vanishes to rounding
@@ -672,11 +672,14 @@ PCD_DEV void jacobi_rot(float (&a)[3][3], float (&V)[3][3]) {
     }
 }
 // Ascending eigenvalues w of T and the eigenvector y of w[0] (unit length, arbitrary sign).
+#ifndef PCD_JACOBI_SWEEPS
+#define PCD_JACOBI_SWEEPS 3   // (4 measured: NVT2 +0.014 ms, same classes in every parity test)
+#endif
 PCD_DEV void eigh3_min(const Sym3& T, float w[3], Vec3& y) {
     float a[3][3] = {{T.a00, T.a01, T.a02}, {T.a01, T.a11, T.a12}, {T.a02, T.a12, T.a22}};
     float V[3][3] = {{1.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, {0.f, 0.f, 1.f}};
 #pragma unroll
-    for (int sweep = 0; sweep < 4; ++sweep) {
+    for (int sweep = 0; sweep < PCD_JACOBI_SWEEPS; ++sweep) {
         jacobi_rot<0, 1, 2>(a, V);
         jacobi_rot<0, 2, 1>(a, V);
         jacobi_rot<1, 2, 0>(a, V);
