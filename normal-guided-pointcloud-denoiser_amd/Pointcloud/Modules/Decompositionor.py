@@ -1,7 +1,8 @@
 """Normal voting tensors (drop-in for Pointcloud/Modules/Decompositionor.py, hot-path subset).
 
 getBetterFilteredNVT -> pcd_nvt_csr: per segment, gather (v_j, n_j), threshold, accumulate the 6 unique entries of
-T, Σw = 0 fallback, in-register 3x3 Jacobi eigen-decomposition (reference Decompositionor.py:278-300).
+T, Σw = 0 fallback, in-register 3x3 eigen-decomposition restating LAPACK ssyevd (ssytd2 + ssteqr, the signs MKL's
+torch.linalg.eigh produces; reference Decompositionor.py:278-300).
 Decomposition.getVUSmoothedNormals -> pcd_vu_smooth (:92-106); getNVTFeatures / getClasses -> pcd_classify (:57-69).
 CPSD path: getNormalFilteredNVT -> pcd_nvt_normal_csr (:260-276), getNormalFilteredPVT -> pcd_pvt_normal_csr
 (:172-211), Decomposition.getVUFeatures (:84-85).

@@ -2,7 +2,7 @@
 
 getKNNEdgeIndex(k) -> kNN of the CURRENT positions over a fresh grid, self excluded (torch_cluster.knn_graph,
 flow="target_to_source", GraphBuilder.py:60-63); getPVTDecompositionWithKNN -> pcd_pca_dense (covariance about the
-neighbours' mean + Jacobi eigh, :99-111); flipNormals -> pcd_orient_normals_mst_gpu (Borůvka MST + Euler-tour
+neighbours' mean + the LAPACK-ssyevd 3x3 eigh, :99-111); flipNormals -> pcd_orient_normals_mst_gpu (Borůvka MST + Euler-tour
 rooting + sign pointer jumping on the device, :129-209; bit-identical to the host Kruskal + DFS pcd_orient_normals_mst,
 which the tests keep as the cross-check).
 """
