@@ -183,6 +183,8 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="N > 1 slabs: one global cloud of --points in total (strong scaling, BASELINE configs[4] "
                          "asks for 80M), instead of --points per GPU")
+    ap.add_argument("--no-rebalance", dest="rebalance", action="store_false",
+                    help="slab mode: keep the equal-count cut (default: re-cut by class cost after warm-up 2)")
     ap.add_argument("--no-ten", dest="ten", action="store_false",
                     help="skip the ten_iteration_ms measurement (fresh cloud, 10 iterations incl. the first)")
     args = ap.parse_args()
@@ -208,14 +210,23 @@ def main():
         # one global cloud of world x P points (identical on every rank), cut into spatial slabs with a halo
         from pcd_slab import SlabDenoiser, TorchTransport
         total = args.points if args.strong else args.points * world
-        pos, nrm, diag = make_cloud(total, 3, dev)
-        dist.broadcast(pos, 0)       # one cloud: rank 0's (device sampling is not bit-reproducible across ranks)
+        # one cloud, sampled on rank 0 only and broadcast (device sampling is not bit-reproducible across ranks);
+        # d = 2 l (Processor.py:120-121) likewise on rank 0 only: the other ranks never grid the whole cloud
+        if rank == 0:
+            pos, nrm, diag = make_cloud(total, 3, dev)
+            dt = torch.tensor([2 * float(Processor(Pointcloud(pos), k_hint=args.k).meanEdgeLength())], device=dev)
+        else:
+            pos = torch.empty((total, 3), dtype=torch.float32, device=dev)
+            nrm = torch.empty_like(pos)
+            dt = torch.zeros(1, device=dev)
+        dist.broadcast(pos, 0)
         dist.broadcast(nrm, 0)
-        dt = torch.tensor([2 * float(Processor(Pointcloud(pos), k_hint=args.k).meanEdgeLength())], device=dev)
         dist.broadcast(dt, 0)
         d = float(dt)
+        # coverage checked every 10 iterations (a thin halo re-plans and replays, pcd_slab); slabs re-cut by class
+        # cost after the second warm-up iteration (rebalance), so the timed region runs on the balanced plan
         sd = SlabDenoiser(pos, nrm, max(args.k, args.k_update), transport=TorchTransport(), k_hint=args.k,
-                          seeding=args.seeding)
+                          seeding=args.seeding, check_every=10)
         del pos, nrm
         params = nat.make_params(k=args.k, k_update=args.k_update, d=d)
         step = lambda: sd.iterate(params, 1)  # noqa: E731
@@ -241,6 +252,8 @@ def main():
             first_ms = (time.perf_counter() - tf) * 1e3
         else:
             step()
+        if mode == "slab" and args.rebalance and w == min(1, args.warmup - 2):
+            sd.rebalance()         # cost-weighted cut from this iteration's classes (next iteration re-anchors)
     if mode != "slab":
         fused.set_timing(True)     # per-stage HIP events on the launch stream, every timed iteration
     torch.cuda.synchronize()

@@ -119,6 +119,13 @@ int pcd_vu_smooth(const float* eigval, const float* eigvec, const float* n, int6
                   float* out, void* stream);
 /* features nullable [m][3] = (planarity, linearity, sphericity); classes int64 [m] */
 int pcd_classify(const float* eigval, int64_t m, float scale, float* features, int64_t* classes, void* stream);
+/* The kernels' two 3x3 symmetric eigen-solvers on DEVICE tensors t6 [m][6] = (a00, a01, a02, a11, a12, a22), as
+ * the fused loop compiles them (torch.linalg.eigh at Decompositionor.py:300 is what both replace):
+ *   solver 0: the LAPACK ssyevd restatement (NVT1, the public ops) -> w [m][3] ascending, vec [m][3][3] columns
+ *   solver 1: NVT2's fixed-sweep Jacobi on the hardware rcp/sqrt estimates -> w [m][3] ascending, vec [m][3] = the
+ *             smallest eigenvalue's unit eigenvector (sign arbitrary; classes and edge_step use it through y yᵀ)
+ * For tests: pins NVT2's solver against the LAPACK one on the same tensors. */
+int pcd_eigh3_batch(const float* t6, int64_t m, int solver, float* w, float* vec, void* stream);
 /* Covariance of the k neighbours nbr[i*k .. i*k+k) about their own mean; eigval [n][3], eigvec [n][3][3]. */
 int pcd_pca_dense(const float* pos, int64_t n, const int64_t* nbr, int k, float* eigval, float* eigvec,
                   void* stream);
@@ -168,6 +175,9 @@ typedef struct {
                             (PostProcessing.ipynb:1088-1089, mask = ||temp_pos - original_pos|| < d); 0: off */
 } pcd_denoise_params;
 
+/* sizeof(pcd_denoise_params) as this library was built: a binding checks its mirror against it (a struct that
+ * is shorter than the library's would be read past its end). */
+int pcd_denoise_params_size(void);
 /* g: the frozen snapshot, at most 2^28 points (268M; larger clouds run as spatial slabs, pcd_slab). */
 int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out);
 int pcd_denoiser_destroy(pcd_denoiser* dn);
@@ -210,10 +220,20 @@ int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n
 /* Device error word -> status: PCD_ERR_STATE if a kNN list held an invalid entry or (spatial slabs) a query's
  * k-ball left the coverage box.  Synchronises `stream`.  store() calls it. */
 int pcd_denoiser_check(pcd_denoiser* dn, void* stream);
+/* The raw device error word behind check (bit 0: invalid list entry, bit 1: a k-ball left the coverage box), without
+ * raising: the spatial-slab driver widens its halo and re-plans on bit 1.  Synchronises `stream`. */
+int pcd_denoiser_status(pcd_denoiser* dn, int* bits, void* stream);
 /* The kNN list the last K1 stage stored (the snapshot's `cols` nearest of each point's current position, in
  * (distance, index) order = getKNNSelection's columns, Selector.py:235-246), in caller order with ORIGINAL snapshot
  * indices: out int64 [N][cols], cols <= the stored list length (max(k, k_update) of the last iteration). */
 int pcd_denoiser_lists(pcd_denoiser* dn, int64_t* out, int cols, void* stream);
+/* Parity probe of the fused NVT2 stage (off by default; enabling allocates [N] float4).  While on, every NVT2 stage
+ * also writes, per row, the eigenvalues of the reference's normalised tensor T / Σw (Decompositionor.py:299-300:
+ * getBetterFilteredNVT's eigval, ascending) and Σw, as that kernel computes them.  probe_store copies them out in
+ * caller order: nvt2_eig4 [N][4] = (λ0, λ1, λ2, Σw); rows no NVT2 stage wrote hold NaN.  The edge vectors (the
+ * smallest eigenvalue's eigenvector) come out through pcd_denoiser_store. */
+int pcd_denoiser_set_probe(pcd_denoiser* dn, int enable);
+int pcd_denoiser_probe_store(pcd_denoiser* dn, float* nvt2_eig4, void* stream);
 
 /* ---- spatial slabs (multi-GPU): the same loop over a rank's own points with a halo ----
  * The grid holds the rank's points plus halo snapshot points owned by other ranks.  Only the ACTIVE rows are

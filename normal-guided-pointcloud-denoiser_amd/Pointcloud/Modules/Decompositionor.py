@@ -49,7 +49,10 @@ class Decomposition:
         return (self.eigval < tau).sum(dim=1) % 3
 
     def getVUSmoothedNormals(self, n: torch.Tensor, tau: float = 0.3, d: float = 3):
-        """normalize(d·n + Σ_k [λ_k > τ] (e_k·n) e_k)."""
+        """Decompositionor.py:92-106 as the reference writes it: f_n = normalize(d·n + Eᵀ·M·E·n), with E[r][k] the r-th
+        component of the k-th eigenvector in descending eigenvalue order and M = diag([λ_(r) > τ]) indexed by that
+        rank (NOT the projector Σ_k [λ_k > τ] (e_k·n) e_k = E·M·Eᵀ·n: the two agree only for M = 0 or I, so the
+        result depends on LAPACK's eigenvector signs -- pcd_device.h vu_smooth)."""
         out = _nat.vu_smooth(_nat.f32(self.eigval), _nat.f32(self.eigvec), _nat.f32(n), tau, d)
         return out.to(n.device)
 

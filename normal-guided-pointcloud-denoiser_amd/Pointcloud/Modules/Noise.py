@@ -34,7 +34,8 @@ class Noise:
                         dtype=torch.float32).to(gt.device) * std
         offset = r if noise_direction == 1 else self.graph.n * r[:, 0, None]
         if noise_type == 1:
-            drop = torch.randperm(n, generator=generator)[:int(n * (1 - noise_level))].to(gt.device)
+            gdev = gt.device if generator is None else generator.device
+            drop = torch.randperm(n, generator=generator, device=gdev)[:int(n * (1 - noise_level))].to(gt.device)
             offset[drop] = 0
         self.setNoise(gt + offset, keepNormals)
 

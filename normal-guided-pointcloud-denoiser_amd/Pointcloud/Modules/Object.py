@@ -99,9 +99,10 @@ class Pointcloud:
         assert path.suffix == ".obj"
         v, _, fv, _ = read_obj_arrays(file_path)
         assert v.shape[1] == 3 and fv.shape[1] == 3
-        pos, nrm = sample_surface(torch.tensor(v, dtype=torch.float32), torch.tensor(fv), num_points,
-                                  generator=generator)
-        pc = Pointcloud(pos.to(device), nrm.to(device))
+        # sampled where the cloud will live (the 10M / 80M bench clouds are drawn on the GPU, never through host RAM)
+        pos, nrm = sample_surface(torch.tensor(v, dtype=torch.float32, device=device),
+                                  torch.tensor(fv, device=device), num_points, generator=generator)
+        pc = Pointcloud(pos, nrm)
         pc.file_path = file_path
         return pc
 

@@ -440,7 +440,7 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
         if (!DENSE) {
             const float4 a = anc[i];
             // (D + |q - a|)² bounds the KA-th key at q only for a FULL anchor set (KA points within D of a); a partial
-            // set (fewer points within its radius, unused slots -1) gives no such bound
+            // set (fewer points within its radius, unused slots = N, the +inf sentinel row) gives no such bound
             if (a.w >= 0.f && (uint32_t)alist[(int64_t)(KA - 1) * N + i] < (uint32_t)N) cap = anchor_cap(q, a);
         }
         const unsigned long long top = wave_knn<KA>(g, q, cap, s_buf[wv], &s_cells[wv], lane);
@@ -471,7 +471,7 @@ template <int K>
 __global__ __launch_bounds__(kNvtBS) void k_nvt2(const float4* __restrict__ pos, const float4* __restrict__ fn,
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                float rho, float scale, uint8_t* __restrict__ cls,
-                                               float4* __restrict__ edge, int win) {
+                                               float4* __restrict__ edge, int win, float4* __restrict__ probe) {
     __shared__ float4 s_pos[WinSize<kWinHaloNvt2, kNvtBS>::rows], s_fn[WinSize<kWinHaloNvt2, kNvtBS>::rows];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
     const int64_t lo = stage_window<kWinHaloNvt2, kNvtBS>(pos, fn, N, rm(b0), s_pos, s_fn, win);
@@ -481,20 +481,27 @@ __global__ __launch_bounds__(kNvtBS) void k_nvt2(const float4* __restrict__ pos,
     const float4 p4 = pos[i];
     // classes and the edge vector are invariant to the positive scale 1/Σw (ratios of eigenvalues, a unit
     // eigenvector): the tensor is left unnormalised.  f_n is NVT1's normalised output: the vote margin is constant.
+    int wsum = 0;
     const Sym3 T = nvt_tensor<K, PCD_NVT2_NORM, true>(WinRows<kWinHaloNvt2, kNvtBS>{pos, s_pos, lo}, WinRows<kWinHaloNvt2, kNvtBS>{fn, s_fn, lo},
-                                                v3(p4.x, p4.y, p4.z), k, ColNbStream{idx, N, i}, rho, ColNbSafe{idx, N, i});
+                                                v3(p4.x, p4.y, p4.z), k, ColNbStream{idx, N, i}, rho, ColNbSafe{idx, N, i},
+                                                probe ? &wsum : nullptr);
 #ifdef PCD_NVT2_LAPACK
     float w[3], V[3][3];
     eigh3(T, w, V);
-    cls[i] = (uint8_t)classify(w, scale, nullptr);
-    store4(edge, i, v3(V[0][0], V[1][0], V[2][0]));
+    const Vec3 y = v3(V[0][0], V[1][0], V[2][0]);
 #else
     float w[3];
     Vec3 y;
     eigh3_min(T, w, y);
+#endif
     cls[i] = (uint8_t)classify(w, scale, nullptr);
     store4(edge, i, y);
-#endif
+    // parity probe (pcd_denoiser_set_probe): the eigenvalues of the reference's normalised tensor T / Σw
+    // (Decompositionor.py:299-300) as this kernel computes them, and Σw
+    if (probe) {
+        const float c = PCD_NVT2_NORM ? 1.f : (float)wsum;
+        probe[i] = make_float4(w[0] / c, w[1] / c, w[2] / c, (float)wsum);
+    }
 }
 
 struct RedC { double sx, sy, sz, cnt; };
@@ -664,6 +671,13 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     store4(pout, i, o);
 }
 
+// sorted-order float4 rows -> caller order (the probe)
+__global__ void k_scatter4(const float4* __restrict__ src, const int32_t* __restrict__ perm, int64_t N,
+                           float4* __restrict__ out) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r < N) out[perm[r]] = src[r];
+}
+
 // pcd_denoiser_lists: column-major sorted-order lists -> caller rows of original indices
 __global__ void k_lists(const int32_t* __restrict__ idx, const int32_t* __restrict__ perm, int64_t N, int cols,
                         int64_t* __restrict__ out) {
@@ -725,6 +739,7 @@ struct pcd_denoiser {
     bool anchoring = true;        // anchored kNN for seeded searches (pcd_denoiser_set_anchoring)
     bool unit_nrm = false;        // nrm holds the loop's own normalised f_n (set by finish, cleared by load / writes)
     int windows = 1;              // LDS row windows in NVT1 / NVT2 / the flat phase (pcd_denoiser_set_windows)
+    float4* probe = nullptr;      // NVT2 parity probe (pcd_denoiser_set_probe): normalised eigenvalues + Σw per row
     bool loaded = false, iterated = false;
     bool timing = false;
     std::vector<hipEvent_t> ev;   // kTimingSets sets of kTimingEvents events, one set per timed iteration
@@ -919,7 +934,7 @@ static int stage_k2(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t s
     float4* P = dn->pos[dn->cur];
 #define PCD_K2(C) \
     case C:                                                                                                            \
-        hipLaunchKernelGGL((k_nvt2<C>), grd, blk, 0, st, P, dn->fn, dn->idx, dn->n, rm, p->k, p->rho, p->class_scale, dn->cls, dn->edge, dn->windows); \
+        hipLaunchKernelGGL((k_nvt2<C>), grd, blk, 0, st, P, dn->fn, dn->idx, dn->n, rm, p->k, p->rho, p->class_scale, dn->cls, dn->edge, dn->windows, dn->probe); \
         break;
     switch (list_cap(p)) {
         PCD_K2(8) PCD_K2(16) PCD_K2(32) PCD_K2(64)
@@ -1062,7 +1077,7 @@ int pcd_denoiser_destroy(pcd_denoiser* dn) {
     (void)hipFree(dn->edge); (void)hipFree(dn->orig); (void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part);
     (void)hipFree(dn->red); (void)hipFree(dn->gscal); (void)hipFree(dn->err);
     (void)hipFree(dn->anc); (void)hipFree(dn->alist); (void)hipFree(dn->redo); (void)hipFree(dn->spill);
-    (void)hipFree(dn->rqs); (void)hipFree(dn->fail); (void)hipFree(dn->sel_tmp);
+    (void)hipFree(dn->rqs); (void)hipFree(dn->fail); (void)hipFree(dn->sel_tmp); (void)hipFree(dn->probe);
     if (dn->side) (void)hipStreamDestroy(dn->side);
     if (dn->fork) (void)hipEventDestroy(dn->fork);
     if (dn->join) (void)hipEventDestroy(dn->join);
@@ -1163,6 +1178,13 @@ int pcd_denoiser_check(pcd_denoiser* dn, void* stream) {
     return PCD_OK;
 }
 
+int pcd_denoiser_status(pcd_denoiser* dn, int* bits, void* stream) {
+    PCD_CHECK_ARG(dn && bits, "null argument");
+    PCD_HIP(hipMemcpyAsync(bits, dn->err, sizeof(int), hipMemcpyDeviceToHost, as_stream(stream)));
+    PCD_HIP(hipStreamSynchronize(as_stream(stream)));
+    return PCD_OK;
+}
+
 int pcd_denoiser_lists(pcd_denoiser* dn, int64_t* out, int cols, void* stream) {
     PCD_CHECK_ARG(dn && out, "null argument");
     PCD_CHECK_ARG(dn->iterated && cols >= 1 && cols <= dn->list_cols, "cols must be in [1, stored list length]");
@@ -1221,6 +1243,29 @@ int pcd_denoiser_set_anchoring(pcd_denoiser* dn, int enable) {
 int pcd_denoiser_set_windows(pcd_denoiser* dn, int enable) {
     PCD_CHECK_ARG(dn != nullptr, "null denoiser");
     dn->windows = enable != 0;
+    return PCD_OK;
+}
+
+int pcd_denoiser_set_probe(pcd_denoiser* dn, int enable) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    if (!enable) {
+        (void)hipFree(dn->probe);
+        dn->probe = nullptr;
+        return PCD_OK;
+    }
+    if (!dn->probe) {
+        if (hipMalloc(&dn->probe, dn->n * sizeof(float4)) != hipSuccess) return fail(PCD_ERR_OOM, "pcd_denoiser: probe");
+        PCD_HIP(hipMemset(dn->probe, 0xFF, dn->n * sizeof(float4)));   // NaN until an NVT2 stage writes a row
+    }
+    return PCD_OK;
+}
+
+int pcd_denoiser_probe_store(pcd_denoiser* dn, float* nvt2_eig4, void* stream) {
+    PCD_CHECK_ARG(dn && nvt2_eig4, "null argument");
+    PCD_CHECK_ARG(dn->probe != nullptr, "probe not enabled (pcd_denoiser_set_probe)");
+    hipLaunchKernelGGL(k_scatter4, dim3((unsigned)cdiv(dn->n, 256)), dim3(256), 0, as_stream(stream), dn->probe,
+                       dn->g->perm, dn->n, reinterpret_cast<float4*>(nvt2_eig4));
+    PCD_LAUNCH_CHECK();
     return PCD_OK;
 }
 

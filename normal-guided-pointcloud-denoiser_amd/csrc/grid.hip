@@ -307,6 +307,7 @@ extern "C" {
 const char* pcd_last_error(void) { return g_last_error.c_str(); }
 int pcd_version(void) { return 1; }
 int pcd_max_k(void) { return 64; }
+int pcd_denoise_params_size(void) { return (int)sizeof(pcd_denoise_params); }
 
 // bbox + cell edge of a point set (the part of the build that fixes the cell lattice).
 static int grid_lattice(const float* xyz, int64_t n, int k_hint, float cell, hipStream_t st, float mn[3], float mx[3],

@@ -36,6 +36,33 @@ __global__ __launch_bounds__(256) void k_nvt_csr(Rows3 pos, Rows3 nrm, const int
         for (int b = 0; b < 3; ++b) eigvec[9 * r + 3 * a + b] = V[a][b];
 }
 
+// The two device eigen-solvers on caller tensors (pcd_eigh3_batch): SOLVER 0 = eigh3 (the LAPACK ssyevd restatement
+// NVT1 and the public ops run), 1 = eigh3_min (NVT2's fixed-sweep Jacobi on the hardware estimates, as k_nvt2
+// compiles it).  t6 [m][6] = (a00, a01, a02, a11, a12, a22); vec: [m][3][3] columns (0) or the smallest's [m][3] (1).
+template <int SOLVER>
+__global__ __launch_bounds__(256) void k_eigh3_batch(const float* __restrict__ t6, int64_t m, float* __restrict__ w,
+                                                      float* __restrict__ vec) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    const float* t = t6 + 6 * r;
+    const Sym3 T{t[0], t[1], t[2], t[3], t[4], t[5]};
+    float ww[3];
+    if constexpr (SOLVER == 0) {
+        float V[3][3];
+        eigh3(T, ww, V);
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) vec[9 * r + 3 * a + b] = V[a][b];
+    } else {
+        Vec3 y;
+        eigh3_min(T, ww, y);
+        store3(vec, r, y);
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) w[3 * r + a] = ww[a];
+}
+
 // CPSD tensors over a CSR selection (KIND 0: normal-filtered NVT, 1: normal-filtered PVT) + eigh.
 template <int KIND>
 __global__ __launch_bounds__(256) void k_cpsd_csr(Rows3 pos, Rows3 nrm, const int64_t* __restrict__ ci,
@@ -194,6 +221,17 @@ int pcd_nvt_csr(const float* pos, const float* n, int64_t npts, const int64_t* c
     PCD_CHECK_ARG(npts > 0, "empty point set");
     hipLaunchKernelGGL(k_nvt_csr, dim3((unsigned)cdiv(m, 256)), dim3(256), 0, as_stream(stream), Rows3{pos},
                        Rows3{n}, ci, off, nbr, m, rho, eigval, eigvec);
+    PCD_LAUNCH_CHECK();
+    return PCD_OK;
+}
+
+int pcd_eigh3_batch(const float* t6, int64_t m, int solver, float* w, float* vec, void* stream) {
+    PCD_CHECK_ARG(solver == 0 || solver == 1, "solver must be 0 (LAPACK restatement) or 1 (NVT2 Jacobi)");
+    if (m == 0) return PCD_OK;
+    PCD_CHECK_ARG(t6 && w && vec, "null argument");
+    const dim3 grd((unsigned)cdiv(m, 256)), blk(256);
+    if (solver == 0) hipLaunchKernelGGL(k_eigh3_batch<0>, grd, blk, 0, as_stream(stream), t6, m, w, vec);
+    else hipLaunchKernelGGL(k_eigh3_batch<1>, grd, blk, 0, as_stream(stream), t6, m, w, vec);
     PCD_LAUNCH_CHECK();
     return PCD_OK;
 }

@@ -62,9 +62,10 @@ PCD_DEV void for_neighbours(P pos, Nr nrm, int cnt, Nb nb, F&& f) {
 // (1 + |n_j|₁)² <= (1 + √3 (1 + 1e-6))² < 7.47 and the margin is the constant kUnitMargin·sq.
 static constexpr float kVoteEps = 4e-6f;
 static constexpr float kUnitMargin = kVoteEps * 7.47f;
+// wsum_out (nullable): Σ w after the fallback (the divisor of NORM; the NVT2 probe reports it).
 template <int UNROLL = 0, bool NORM = true, bool UNIT = false, int BATCH = kNbBatch, class P, class Nr, class Nb,
           class NbF>
-PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF nbf) {
+PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF nbf, int* wsum_out = nullptr) {
     float w00 = 0.f, w01 = 0.f, w02 = 0.f, w11 = 0.f, w12 = 0.f, w22 = 0.f;
     int wsum = 0;
     const float cthr = cosf(rho);
@@ -123,6 +124,7 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF n
         }
         wsum = cnt;
     }
+    if (wsum_out) *wsum_out = wsum;
     if (!NORM) return Sym3{w00, w01, w02, w11, w12, w22};
     const float c = (float)wsum;
     return Sym3{w00 / c, w01 / c, w02 / c, w11 / c, w12 / c, w22 / c};

@@ -442,7 +442,7 @@ PCD_DEV bool rq_query(const GridView& g, const Src& src, int64_t i, Vec3 q, floa
         }
         return true;
     }
-    // this lane's elements hl and W + hl of the order; unused slots of a partial set hold -1 (the anchor test
+    // this lane's elements hl and W + hl of the order; unused slots of a partial set hold N, the snapshot's +inf sentinel row (the anchor test
     // gives them an infinite distance)
     const int e0 = lg.hl, e1 = W + lg.hl;
     const bool h0 = e0 < KA && e0 < cnt, h1 = e1 < KA && e1 < cnt;

@@ -44,6 +44,7 @@ _SIGS = {
     "pcd_last_error": (ctypes.c_char_p, []),
     "pcd_version": (c_int, []),
     "pcd_max_k": (c_int, []),
+    "pcd_denoise_params_size": (c_int, []),
     "pcd_grid_build": (c_int, [c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, POINTER(c_void_p)]),
     "pcd_grid_params": (c_int, [c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, c_void_p]),
     "pcd_grid_destroy": (c_int, [c_void_p]),
@@ -62,6 +63,7 @@ _SIGS = {
     "pcd_vu_smooth": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p, c_void_p]),
     "pcd_classify": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p, c_void_p]),
     "pcd_pca_dense": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "pcd_eigh3_batch": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "pcd_step_csr": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
                              c_float, c_float, c_void_p, c_void_p]),
     "pcd_edge_length_sum": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
@@ -80,7 +82,10 @@ _SIGS = {
     "pcd_denoiser_anchor_stats": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_denoiser_tile_stats": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_denoiser_check": (c_int, [c_void_p, c_void_p]),
+    "pcd_denoiser_status": (c_int, [c_void_p, POINTER(c_int), c_void_p]),
     "pcd_denoiser_lists": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "pcd_denoiser_set_probe": (c_int, [c_void_p, c_int]),
+    "pcd_denoiser_probe_store": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_denoiser_set_rows": (c_int, [c_void_p, c_void_p, c_int64]),
     "pcd_denoiser_set_coverage": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_denoiser_stage": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
@@ -110,6 +115,10 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        # the params mirror must match the library's struct (a shorter one would be read past its end)
+        if ctypes.sizeof(DenoiseParams) != L.pcd_denoise_params_size():
+            raise ImportError(f"pcd: DenoiseParams mirror is {ctypes.sizeof(DenoiseParams)} B, the library's "
+                              f"pcd_denoise_params is {L.pcd_denoise_params_size()} B -- rebuild or update the mirror")
         _lib = L
     return _lib
 
@@ -279,6 +288,16 @@ class FusedDenoiser:
         check(lib().pcd_denoiser_lists(self.handle, ptr(out), int(cols), c_void_p(stream_ptr())), "pcd_denoiser_lists")
         return out
 
+    def set_probe(self, enable=True):
+        """NVT2 parity probe on / off (pcd_denoiser_set_probe)."""
+        check(lib().pcd_denoiser_set_probe(self.handle, int(bool(enable))), "pcd_denoiser_set_probe")
+
+    def probe(self) -> torch.Tensor:
+        """(λ0, λ1, λ2, Σw) of the last NVT2 stage per point, caller order: float32 [N, 4]."""
+        out = torch.empty((self.grid.n, 4), dtype=torch.float32, device=device())
+        check(lib().pcd_denoiser_probe_store(self.handle, ptr(out), c_void_p(stream_ptr())), "pcd_denoiser_probe_store")
+        return out
+
     def set_seeding(self, enable=True):
         check(lib().pcd_denoiser_set_seeding(self.handle, int(bool(enable))), "pcd_denoiser_set_seeding")
 
@@ -309,6 +328,12 @@ class FusedDenoiser:
 
     def check(self):
         check(lib().pcd_denoiser_check(self.handle, c_void_p(stream_ptr())), "pcd_denoiser_check")
+
+    def status(self) -> int:
+        """Device error word (bit 0: invalid list entry, bit 1: a k-ball left the coverage box), not raising."""
+        v = c_int(0)
+        check(lib().pcd_denoiser_status(self.handle, ctypes.byref(v), c_void_p(stream_ptr())), "pcd_denoiser_status")
+        return v.value
 
     # ---- spatial slabs: active rows, coverage, staged iteration, halo pack/unpack (include/pcd.h)
     @staticmethod
@@ -432,6 +457,18 @@ def pca_dense(pos, nbr, k):
     check(lib().pcd_pca_dense(ptr(pos), n, ptr(nbr), int(k), ptr(ev), ptr(evec), c_void_p(stream_ptr())),
           "pcd_pca_dense")
     return ev, evec
+
+
+def eigh3_batch(t6, solver=0):
+    """Device eigen-solvers of the kernels on t6 (m, 6): solver 0 (LAPACK restatement) -> (w (m,3), V (m,3,3));
+    solver 1 (NVT2's Jacobi) -> (w (m,3), y (m,3))."""
+    t = f32(t6)
+    assert t.dim() == 2 and t.size(1) == 6
+    m = t.size(0)
+    w = torch.empty((m, 3), dtype=torch.float32, device=t.device)
+    vec = torch.empty((m, 3, 3) if solver == 0 else (m, 3), dtype=torch.float32, device=t.device)
+    check(lib().pcd_eigh3_batch(ptr(t), m, int(solver), ptr(w), ptr(vec), c_void_p(stream_ptr())), "pcd_eigh3_batch")
+    return w, vec
 
 
 def step_csr(kind, pos, n, edge_vectors, ci, off, nbr, d, alpha):

@@ -14,7 +14,14 @@ rows current between stages (the only places a stage reads another rank's points
     FINISH                          n := f_n (the halo rows' f_n arrived with the FN exchange)
 The global flat centre / delta (Denoiser.py:106-107) are the only collectives; halo traffic is point-to-point
 between slab neighbours.  Exactness is checked, not assumed: every k-ball must stay inside the slab widened by the
-halo (pcd_denoiser_set_coverage), otherwise check() raises (halo too thin).
+halo (pcd_denoiser_set_coverage).  Every `check_every` iterations the driver reads the device error word (one host
+sync and a 1-int all-reduce); when a k-ball has left a rank's coverage it restores the state of the last checkpoint,
+widens the halo (x `halo_growth`), re-plans every rank from the frozen snapshot and replays the iterations since the
+checkpoint -- the result is the one a wide-enough halo gives from the start.
+
+Slabs are cut at quantiles of a per-point COST weight (default 1 = equal counts).  rebalance() re-plans with weights
+from the last iteration's classes (edge / corner points run the dearer 3x3-solve steps), the same machinery as the
+thin-halo re-plan.
 
 The driver is engine-agnostic: `HipSlabEngine` (libpcd, the product path) or any object with the same methods
 (the CPU tests use an oracle engine, tests/slab_cpu_engine.py).
@@ -42,7 +49,10 @@ class SlabPlan:
     local: list = field(default_factory=list)   # per rank: int64 global indices of owned + halo, ascending
 
     @staticmethod
-    def build(snap: torch.Tensor, world: int, halo: float, axis: int | None = None) -> "SlabPlan":
+    def build(snap: torch.Tensor, world: int, halo: float, axis: int | None = None,
+              weights: torch.Tensor | None = None) -> "SlabPlan":
+        """weights (optional, [N] >= 0, identical on every rank): cut at quantiles of the cumulative weight along the
+        axis instead of equal point counts (each rank still owns at least one point)."""
         snap = snap.detach()
         n = snap.size(0)
         assert world >= 1 and n >= world, "need at least one point per rank"
@@ -52,7 +62,16 @@ class SlabPlan:
         key = snap[:, axis].contiguous()
         order = torch.sort(key, stable=True).indices           # ties by index: deterministic on every rank
         owner = torch.empty(n, dtype=torch.int64, device=snap.device)
-        bounds = [(r * n) // world for r in range(world + 1)]
+        if weights is None:
+            bounds = [(r * n) // world for r in range(world + 1)]
+        else:
+            cw = torch.cumsum(weights.to(snap.device, torch.float64)[order], 0)
+            tot = float(cw[-1])
+            cuts = torch.tensor([tot * r / world for r in range(1, world)], dtype=torch.float64, device=snap.device)
+            inner = torch.searchsorted(cw, cuts).tolist() if world > 1 else []
+            bounds = [0] + [int(b) for b in inner] + [n]
+            for r in range(1, world + 1):                       # at least one point per rank, monotone
+                bounds[r] = min(max(bounds[r], bounds[r - 1] + 1), n - (world - r))
         lo, hi, local = [], [], []
         for r in range(world):
             owner[order[bounds[r]:bounds[r + 1]]] = r
@@ -185,6 +204,22 @@ class HipSlabEngine:
     def check(self):
         self.fused.check()
 
+    def status(self) -> int:
+        return self.fused.status()
+
+    def set_state(self, local_idx, pos, n):
+        """Current positions / normals of the given local points (a re-planned rank taking over the state)."""
+        rows = self.rows(local_idx)
+        pad = torch.zeros((rows.numel(), 1), dtype=torch.float32, device=self.device)
+        self.fused.unpack(nat.FIELD_POS, rows, torch.cat([pos.to(self.device, torch.float32), pad], 1))
+        self.fused.unpack(nat.FIELD_NRM, rows, torch.cat([n.to(self.device, torch.float32), pad], 1))
+
+    def classes(self) -> torch.Tensor:
+        """Classes of the last NVT2 stage per local point (int64, local order)."""
+        cls = torch.empty(self.n, dtype=torch.int64, device=self.device)
+        self.fused.store(classes=cls)
+        return cls
+
     def store(self):
         pos = torch.empty((self.n, 3), dtype=torch.float32, device=self.device)
         n = torch.empty_like(pos)
@@ -197,11 +232,14 @@ class SlabDenoiser:
     """The body of Processor.denoise (Processor.py:119-139) over spatial slabs, one rank per GPU.
 
     snap_pos / snap_n: the WHOLE cloud (the frozen snapshot is the initial positions, as in Selector.__init__);
-    rank 0's copy is broadcast, so every rank plans from identical data.  halo: slab widening in snapshot units (None: 3x the largest k-th neighbour distance
-    of a sample, see default_halo)."""
+    rank 0's copy is broadcast, so every rank plans from identical data and keeps it (the frozen snapshot a re-plan
+    cuts again).  halo: slab widening in snapshot units (None: 3x the largest k-th neighbour distance of a sample,
+    see default_halo, estimated on rank 0 and broadcast).  check_every: iterations between coverage checks
+    (0: never -- check() raises at the caller's request instead); halo_growth / max_replans: the thin-halo
+    recovery."""
 
     def __init__(self, snap_pos, snap_n, k_max, transport=None, halo=None, engine_factory=None, seeding=True,
-                 k_hint=32):
+                 k_hint=32, check_every=1, halo_growth=2.0, max_replans=4, weights=None):
         self.t = transport or LocalTransport()
         rank, world = self.t.rank, self.t.world
         if world > 1:
@@ -214,20 +252,44 @@ class SlabDenoiser:
             if rank == 0:
                 h.fill_(default_halo(snap_pos, k_max))
             halo = float(self.t.broadcast_(h)) if world > 1 else float(h)
-        self.plan = SlabPlan.build(snap_pos, world, halo)
-        plan = self.plan
+        self.snap_pos, self.snap_n = snap_pos, snap_n
+        self.k_max, self.k_hint, self.seeding = k_max, k_hint, seeding
+        self.engine_factory = engine_factory
+        self.check_every, self.halo_growth, self.max_replans = int(check_every), float(halo_growth), int(max_replans)
+        self.replans = 0
+        self.e = None
+        self._lattice = None
+        self._setup(SlabPlan.build(snap_pos, world, halo, weights=weights))
+        self._since = 0            # iterations since the last checkpoint
+        self._pending = []         # their params (replayed after a re-plan)
+        self._ckpt = None
+
+    # -------------------------------------------------------------------------------- plan -> engine + routes
+    def _setup(self, plan, state=None):
+        """Build this rank's engine and halo routes for `plan`; state = (global pos, global n) of the CURRENT
+        iterate to take over (None: the snapshot itself, i.e. a fresh start)."""
+        rank, world = self.t.rank, self.t.world
+        self.plan = plan
         self.local = plan.local[rank]                           # global ids, ascending
-        pos_l, n_l = snap_pos[self.local], snap_n[self.local]
+        pos_l, n_l = self.snap_pos[self.local], self.snap_n[self.local]
         owned_mask = plan.owner[self.local] == rank
         self.owned_local = torch.nonzero(owned_mask).flatten()
         self.owned_global = self.local[self.owned_local]
-        if engine_factory is None:
-            origin, cell = nat.grid_params(snap_pos.to(nat.device()), k_hint=k_hint)
-            self.e = HipSlabEngine(pos_l, n_l, self.owned_local, k_max, origin, cell, plan.coverage(rank), seeding)
+        self.e = None                                           # free the old engine's device state first
+        if self.engine_factory is None:
+            if self._lattice is None:
+                self._lattice = nat.grid_params(self.snap_pos.to(nat.device()), k_hint=self.k_hint)
+            origin, cell = self._lattice
+            self.e = HipSlabEngine(pos_l, n_l, self.owned_local, self.k_max, origin, cell, plan.coverage(rank),
+                                   self.seeding)
         else:
-            self.e = engine_factory(pos_l, n_l, self.owned_local, k_max, plan.coverage(rank))
+            self.e = self.engine_factory(pos_l, n_l, self.owned_local, self.k_max, plan.coverage(rank))
+        if state is not None:
+            # the engine loaded the snapshot (its `orig` for the global clamp); the current iterate goes on top
+            lid = torch.arange(self.local.numel(), device=self.local.device)
+            self.e.set_state(lid, state[0][self.local.to(state[0].device)], state[1][self.local.to(state[1].device)])
         # halo routes: rows I send to each peer and rows I receive from it (both ascending global index)
-        to_local = torch.full((snap_pos.size(0),), -1, dtype=torch.int64, device=self.local.device)
+        to_local = torch.full((self.snap_pos.size(0),), -1, dtype=torch.int64, device=self.local.device)
         to_local[self.local] = torch.arange(self.local.numel(), device=self.local.device)
         self.send_rows, self.recv_rows = {}, {}
         for peer in range(world):
@@ -241,6 +303,69 @@ class SlabDenoiser:
                 self.recv_rows[peer] = self.e.rows(to_local[inc])
         self.halo_points = sum(r.numel() for r in self.recv_rows.values())
 
+    def _owned_state_now(self):
+        """(pos, n) of this rank's own points, owned-local order (a checkpoint)."""
+        rows = self.e.rows(self.owned_local)
+        return self.e.pack(nat.FIELD_POS, rows)[:, :3].clone(), self.e.pack(nat.FIELD_NRM, rows)[:, :3].clone()
+
+    def _gather_owned(self, x: torch.Tensor) -> torch.Tensor:
+        """Per-point values of this rank's own points (owned-local order, [n_own, c] float32) -> the global [N, c]
+        on every rank.  Every rank knows the others' owned ids from the plan, so only the values travel (padded
+        all-gather).  Collective."""
+        n_tot = self.snap_pos.size(0)
+        dev = x.device
+        out = torch.empty((n_tot, x.size(1)), dtype=torch.float32, device=dev)
+        if self.t.world == 1:
+            out[self.owned_global.to(dev)] = x
+            return out
+        counts = torch.bincount(self.plan.owner, minlength=self.t.world).tolist()
+        cdev = "cpu" if self.t.host else dev
+        pay = torch.zeros((max(counts), x.size(1)), dtype=torch.float32, device=cdev)
+        pay[: x.size(0)] = x.to(cdev)
+        bufs = [torch.empty_like(pay) for _ in range(self.t.world)]
+        self.t.dist.all_gather(bufs, pay, self.t.group)
+        for r, b in enumerate(bufs):
+            ids = torch.nonzero(self.plan.owner == r).flatten().to(dev)
+            out[ids] = b[: counts[r]].to(dev)
+        return out
+
+    def _global_state(self, owned_pos, owned_n):
+        g = self._gather_owned(torch.cat([owned_pos, owned_n], 1))
+        return g[:, :3], g[:, 3:]
+
+    def _replan(self, halo=None, weights=None, state=None):
+        """Re-cut every rank from the frozen snapshot, taking over `state` (global current pos, n; default: the
+        present iterate).  Collective: all ranks call it together."""
+        if state is None:
+            state = self._global_state(*self._owned_state_now())
+        halo = self.plan.halo if halo is None else halo
+        self._setup(SlabPlan.build(self.snap_pos, self.t.world, halo, axis=self.plan.axis, weights=weights), state)
+
+    def _any_rank(self, flag: bool) -> bool:
+        if self.t.world == 1:
+            return flag
+        dev = "cpu" if self.t.host else self.snap_pos.device
+        f = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+        self.t.all_reduce(f, "max")
+        return bool(f.item())
+
+    def _verify(self):
+        """Coverage check of the iterations since the checkpoint; on a thin halo: restore the checkpoint, widen the
+        halo, re-plan and replay them."""
+        gstate = None
+        while self._any_rank(bool(self.e.status() & 2)):
+            if self.replans >= self.max_replans:
+                raise nat.PcdError(f"pcd_slab: halo still too thin after {self.replans} re-plans "
+                                   f"(halo {self.plan.halo:.4g})")
+            if gstate is None:                  # (the checkpoint is in the order of the plan it was taken under)
+                gstate = self._global_state(*self._ckpt)
+            self._replan(self.plan.halo * self.halo_growth, state=gstate)
+            self.replans += 1
+            for p in self._pending:
+                self._one(p)
+        self._pending = []
+
+    # -------------------------------------------------------------------------------- iteration
     def _exchange(self, fld):
         sends = {p: self.e.pack(fld, rows) for p, rows in self.send_rows.items()}
         shapes = {p: (rows.numel(), 4) for p, rows in self.recv_rows.items()}
@@ -266,16 +391,39 @@ class SlabDenoiser:
             if not params.jacobi:          # Gauss-Seidel: the next phase reads these positions
                 self._exchange(nat.FIELD_POS)
 
-    def iterate(self, params, iterations: int = 1):
+    def _one(self, params):
         e = self.e
+        e.stage(params, nat.STAGE_KNN_NVT1)
+        self._exchange(nat.FIELD_FN)
+        e.stage(params, nat.STAGE_NVT2)
+        self._phases(params)
+        e.stage(params, nat.STAGE_FINISH)
+        if params.jacobi:                  # Jacobi across classes: one position refresh per iteration
+            self._exchange(nat.FIELD_POS)
+
+    def iterate(self, params, iterations: int = 1):
         for _ in range(iterations):
-            e.stage(params, nat.STAGE_KNN_NVT1)
-            self._exchange(nat.FIELD_FN)
-            e.stage(params, nat.STAGE_NVT2)
-            self._phases(params)
-            e.stage(params, nat.STAGE_FINISH)
-            if params.jacobi:              # Jacobi across classes: one position refresh per iteration
-                self._exchange(nat.FIELD_POS)
+            if self.check_every > 0 and self._since == 0:
+                self._ckpt = self._owned_state_now()
+                self._pending = []
+            self._one(params)
+            if self.check_every > 0:
+                self._pending.append(params)
+                self._since += 1
+                if self._since >= self.check_every:
+                    self._verify()
+                    self._since = 0
+
+    def rebalance(self, class_weights=(1.0, 1.3, 1.4)):
+        """Re-cut the slabs by cost: each point weighs class_weights[its class in the last NVT2 stage] (flat, edge,
+        corner: the edge / feature steps solve a 3x3 system over their neighbours).  Collective."""
+        cls = self.e.classes()
+        cls = cls[self.owned_local.to(cls.device)]
+        w_tab = torch.tensor(class_weights, dtype=torch.float32, device=cls.device)
+        w_own = w_tab[cls.clamp(0, len(class_weights) - 1)]
+        weights = self._gather_owned(w_own[:, None])[:, 0].to(self.snap_pos.device)
+        self._replan(weights=weights)
+        self._since, self._pending = 0, []
 
     def iterate_timed(self, params) -> dict:
         """One iteration with CUDA/HIP events on the launch stream around each stage group (ms)."""

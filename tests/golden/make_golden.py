@@ -168,7 +168,6 @@ def gen_fandisk(out_dir):
         cds64.append(chamfer_mean(gt.double(), p64.graph.pos))
         if it in (1, 2, 3, 10):
             res[f"pos64_it{it}"] = p64.graph.pos.numpy().astype(np.float64)
-            res[f"classes64_it{it}"] = np.zeros(1)
     res["cd_f64"] = np.asarray(cds64)
     np.savez_compressed(os.path.join(out_dir, "fandisk_k32.npz"), **res)
     print(f"fandisk_k32: N={N} d={d:.5f} CD {cds[0]:.4g} -> {cds[1]:.4g} {cds[2]:.4g} {cds[3]:.4g} .. {cds[-1]:.4g}"

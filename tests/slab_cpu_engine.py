@@ -116,5 +116,16 @@ class CpuSlabEngine:
         if self.err:
             raise nat.PcdError("halo too thin")
 
+    def status(self):
+        return self.err
+
+    def set_state(self, local_idx, pos, n):
+        li = local_idx.numpy()
+        self.pos[li] = pos.numpy()
+        self.nrm[li] = n.numpy()
+
+    def classes(self):
+        return torch.from_numpy(self.cls.copy())
+
     def store(self):
         return torch.from_numpy(self.pos.copy()), torch.from_numpy(self.nrm.copy())

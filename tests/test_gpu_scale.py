@@ -44,7 +44,8 @@ def bunny_cloud(n, seed, sigma_frac):
 
 
 def run_pair(pos, nrm, k, iterations, dev, check_every=True):
-    """Shipped loop vs the library's reference path on one cloud; returns the redo rows per iteration."""
+    """Shipped loop vs the library's reference path on one cloud; returns the redo rows per iteration.  Both end
+    with pcd_denoiser_check (inside store): a bad list entry would raise."""
     pc = Pointcloud(pos.to(dev), nrm.to(dev))
     proc = Processor(pc, k_hint=k)
     d = 2 * float(proc.meanEdgeLength())
@@ -70,6 +71,8 @@ def run_pair(pos, nrm, k, iterations, dev, check_every=True):
             bad = (pa != pb).any(1) | (na != nb).any(1) | (ca != cb)
             assert not bool(bad.any()), (f"iteration {it}: {int(bad.sum())} of {N} rows differ between the anchored "
                                          f"loop and the unseeded reference path")
+    a.check()
+    b.check()
     return redo, d
 
 
@@ -79,6 +82,17 @@ def test_headline_10m_25_iterations_bitwise(gpu):
     redo, _ = run_pair(pos, nrm, 32, 25, gpu)
     # the re-anchoring path is exercised on every iteration (the dense first one re-anchors every row)
     assert redo[0] == 10_000_000 and min(redo[1:]) > 10_000, redo
+
+
+def test_config5_80m_one_gpu_bitwise(gpu):
+    """BASELINE configs[4]'s whole 80M-point cloud (the bench's slab workload: bench.make_cloud seed 3, sampled on
+    the device) on ONE MI355X: 3 anchored iterations against the reset-seed path (every kNN an unseeded grid
+    search, no LDS windows), state bitwise after every iteration, and the device error word checked at the end
+    (store() runs pcd_denoiser_check: no invalid list entry).  ~75 GB of device state for the pair."""
+    from bench import make_cloud
+    pos, nrm, _ = make_cloud(80_000_000, 3, gpu)
+    redo, _ = run_pair(pos, nrm, 32, 3, gpu)
+    assert redo[0] == 80_000_000 and min(redo[1:]) > 0, redo
 
 
 def _one_iteration_vs_oracle(pos, nrm, k, dev):

@@ -122,6 +122,82 @@ def test_hip_slab_world4_matches_one_gpu(gpu, tmp_path):
     np.testing.assert_allclose(res["n"], rn, rtol=0, atol=1e-5)
 
 
+def _worker_owned(rank, world, port, out_prefix, cloud_path, d, halo=None):
+    """Like _worker, but every rank saves its own points (ids, pos, n) -- no all-gather of the whole cloud."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = np.load(cloud_path)
+        pos, nrm = torch.from_numpy(c["pos"]).to(dev), torch.from_numpy(c["n"]).to(dev)
+        tr = TorchTransport()
+        sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K, halo=halo)
+        del pos, nrm
+        sd.iterate(_params(d), ITERS)
+        sd.check()
+        ids, p, n = sd.owned_state()
+        np.savez(f"{out_prefix}_{rank}.npz", ids=ids.cpu().numpy(), pos=p.cpu().numpy(), n=n.cpu().numpy(),
+                 halo=sd.halo_points, replans=sd.replans)
+    finally:
+        dist.destroy_process_group()
+
+
+def _assemble(prefix, world, n):
+    pos = np.full((n, 3), np.nan, np.float32)
+    nrm = np.full((n, 3), np.nan, np.float32)
+    halos, replans = [], []
+    for r in range(world):
+        z = np.load(f"{prefix}_{r}.npz")
+        pos[z["ids"]] = z["pos"]
+        nrm[z["ids"]] = z["n"]
+        halos.append(int(z["halo"]))
+        replans.append(int(z["replans"]))
+    return pos, nrm, halos, replans
+
+
+@pytest.mark.gpu
+def test_hip_slab_world8_8m_points_matches_one_gpu(gpu, tmp_path):
+    """BASELINE configs[4]'s topology: 8 ranks (6 interior slabs with a halo neighbour on either side) over 8M
+    points, sharing the box's GPU over gloo, against the one-GPU fused loop within 1e-6 x bbox."""
+    import torch.multiprocessing as mp
+    n = 8_000_000
+    pos, nrm = _cloud(gpu, n=n, seed=3)
+    d = _d(pos)
+    prefix, cloud = str(tmp_path / "slab8"), str(tmp_path / "cloud.npz")
+    np.savez(cloud, pos=pos.cpu().numpy(), n=nrm.cpu().numpy())
+    mp.spawn(_worker_owned, args=(8, _free_port(), prefix, cloud, d), nprocs=8, join=True)
+    p, nn, halos, _ = _assemble(prefix, 8, n)
+    assert not np.isnan(p).any() and min(halos) > 0
+    rp, rn = _fused(pos, nrm, d)
+    bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
+    dev = np.abs(p - rp).max()
+    assert dev <= 1e-6 * bbox, dev / bbox
+    np.testing.assert_allclose(nn, rn, rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_hip_slab_world2_thin_halo_replans_and_matches_one_gpu(gpu, tmp_path):
+    """A deliberately thin halo (1/20 of default_halo): the first coverage check fails on both ranks, the driver
+    restores its checkpoint, widens the halo and re-plans from the frozen snapshot, replays -- and ends where the
+    one-GPU fused loop does."""
+    import torch.multiprocessing as mp
+    pos, nrm = _cloud(gpu)
+    d = _d(pos)
+    halo = 0.05 * default_halo(pos, K)
+    prefix, cloud = str(tmp_path / "thin2"), str(tmp_path / "cloud.npz")
+    np.savez(cloud, pos=pos.cpu().numpy(), n=nrm.cpu().numpy())
+    mp.spawn(_worker_owned, args=(2, _free_port(), prefix, cloud, d, halo), nprocs=2, join=True)
+    p, nn, _, replans = _assemble(prefix, 2, pos.size(0))
+    assert min(replans) >= 1
+    rp, rn = _fused(pos, nrm, d)
+    bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
+    np.testing.assert_allclose(p, rp, rtol=0, atol=1e-6 * bbox)
+    np.testing.assert_allclose(nn, rn, rtol=0, atol=1e-5)
+
+
 @pytest.mark.gpu
 def test_hip_slab_world1_jacobi_is_the_fused_loop(gpu):
     """The Jacobi-across-classes mode with the global clamp through the staged engine (one position refresh per

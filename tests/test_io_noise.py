@@ -62,10 +62,17 @@ def test_noise_random_direction_and_keep_normals():
 def test_noise_impulsive_fraction():
     n, level = 100_000, 0.3
     graph = graph_of(n, 4)
-    gt = graph.pos.clone()
+    gt, nrm = graph.pos.clone(), graph.n.clone()
     Noise(graph).generateNoise(level, 0.01, noise_type=1, generator=torch.Generator().manual_seed(5))
-    zero = (graph.pos == gt).all(1)
-    assert int(zero.sum()) == int(n * (1 - level))             # exactly that many offsets zeroed (Noise.py:55-57)
+    # replay the generator: exactly int(n (1 - level)) offsets zeroed (Noise.py:55-57), the rest the Gaussian draws
+    g = torch.Generator().manual_seed(5)
+    r = torch.randn((n, 3), generator=g) * (0.01 * level)
+    drop = torch.randperm(n, generator=g)[:int(n * (1 - level))]
+    keep = torch.ones(n, dtype=torch.bool)
+    keep[drop] = False
+    assert int((~keep).sum()) == int(n * (1 - level))
+    assert torch.equal(graph.pos[~keep], gt[~keep])
+    assert torch.equal(graph.pos[keep], gt[keep] + nrm[keep] * r[keep, 0, None])
 
 
 def test_noise_rejects_out_of_range_and_resets():

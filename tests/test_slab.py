@@ -83,18 +83,27 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_path, halo_scale):
+def _worker(rank, world, port, out_path, halo_scale, opts=None):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    opts = dict(opts or {})
+    rebalance_after = opts.pop("rebalance_after", None)
     try:
         pos, nrm = _cloud()
         params, _ = _params(pos)
         tr = TorchTransport()
         sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, halo=_halo(pos, K) * halo_scale,
-                          engine_factory=CpuSlabEngine)
-        sd.iterate(params, ITERS)
+                          engine_factory=CpuSlabEngine, **opts)
+        owned0 = sd.owned_global.numel()
+        halo0 = sd.plan.halo
+        if rebalance_after is None:
+            sd.iterate(params, ITERS)
+        else:
+            sd.iterate(params, rebalance_after)
+            sd.rebalance(class_weights=(1.0, 3.0, 5.0))
+            sd.iterate(params, ITERS - rebalance_after)
         err = 0
         try:
             sd.check()
@@ -103,21 +112,35 @@ def _worker(rank, world, port, out_path, halo_scale):
         flag = torch.tensor([err], dtype=torch.int64)
         dist.all_reduce(flag)
         p, n = gather_global(sd.owned_state(), pos.size(0), tr)
+        owned = torch.tensor([owned0, sd.owned_global.numel()], dtype=torch.int64)
+        allo = [torch.zeros_like(owned) for _ in range(world)]
+        dist.all_gather(allo, owned)
         if rank == 0:
-            np.savez(out_path, pos=p.numpy(), n=n.numpy(), err=int(flag), halo=sd.halo_points)
+            np.savez(out_path, pos=p.numpy(), n=n.numpy(), err=int(flag), halo=sd.halo_points, replans=sd.replans,
+                     final_halo=sd.plan.halo, halo0=halo0, owned=torch.stack(allo).numpy())
     finally:
         dist.destroy_process_group()
 
 
-def _run_world(tmp_path, halo_scale, world=2):
+def _run_world(tmp_path, halo_scale, world=2, opts=None):
     import torch.multiprocessing as mp
     out = str(tmp_path / f"slab_{world}_{halo_scale}.npz")
-    mp.spawn(_worker, args=(world, _free_port(), out, halo_scale), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, halo_scale, opts), nprocs=world, join=True)
     return np.load(out)
 
 
-def _run_world2(tmp_path, halo_scale):
-    return _run_world(tmp_path, halo_scale, 2)
+def _run_world2(tmp_path, halo_scale, opts=None):
+    return _run_world(tmp_path, halo_scale, 2, opts)
+
+
+def _assert_matches_oracle(res):
+    pos, nrm = _cloud()
+    _, d = _params(pos)
+    rp, rn = _reference(pos, nrm, d)
+    bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
+    # identical per-point arithmetic; only the f64 order of the global flat-centre sum differs across ranks
+    np.testing.assert_allclose(res["pos"], rp, rtol=0, atol=1e-6 * bbox)
+    np.testing.assert_allclose(res["n"], rn, rtol=0, atol=1e-5)
 
 
 def test_slab_world2_gloo_matches_oracle(tmp_path):
@@ -133,8 +156,42 @@ def test_slab_world2_gloo_matches_oracle(tmp_path):
 
 
 def test_slab_world2_thin_halo_is_reported(tmp_path):
-    res = _run_world2(tmp_path, 1e-4)
+    """With the coverage checks off (check_every=0) a thin halo is reported by check(), never silently used."""
+    res = _run_world2(tmp_path, 1e-4, {"check_every": 0})
     assert int(res["err"]) == 2          # both ranks hold a slab face the k-balls cross
+
+
+def test_slab_world2_thin_halo_replans_and_matches_oracle(tmp_path):
+    """A deliberately thin halo (1/20 of the estimate): the driver detects the k-balls leaving the slab, restores the
+    checkpoint, widens the halo (x 3 per re-plan), re-plans both ranks from the frozen snapshot and replays -- and
+    the result is the single-process oracle's."""
+    res = _run_world2(tmp_path, 0.05, {"check_every": 1, "halo_growth": 3.0})
+    assert int(res["err"]) == 0
+    assert int(res["replans"]) >= 1
+    assert float(res["final_halo"]) == pytest.approx(float(res["halo0"]) * 3.0 ** int(res["replans"]), rel=1e-6)
+    _assert_matches_oracle(res)
+
+
+def test_slab_world2_rebalance_by_cost_matches_oracle(tmp_path):
+    """rebalance() after the first iteration re-cuts the slabs by class cost (edge 3x, corner 5x a flat point):
+    ownership moves between ranks and the run still equals the oracle's."""
+    res = _run_world2(tmp_path, 1.0, {"rebalance_after": 1})
+    assert int(res["err"]) == 0
+    owned = res["owned"]                  # per rank: (before, after)
+    assert (owned[:, 0] != owned[:, 1]).any() and owned[:, 1].sum() == owned[:, 0].sum()
+    _assert_matches_oracle(res)
+
+
+def test_plan_weighted_cut():
+    pos, _ = _cloud()
+    w = torch.ones(pos.size(0), dtype=torch.float32)
+    key = pos[:, int(torch.argmax(pos.max(0).values - pos.min(0).values))]
+    w[key > key.median()] = 3.0           # the upper half costs 3x: rank 1 of 2 gets fewer points
+    plan = SlabPlan.build(pos, 2, 0.01, weights=w)
+    counts = torch.bincount(plan.owner, minlength=2)
+    assert counts[1] < counts[0]
+    load = torch.zeros(2).index_add_(0, plan.owner, w)
+    assert abs(float(load[0] - load[1])) <= 2 * 3.0 + 1e-4     # the cut straddles at most one point: 2 w_max
 
 
 def test_slab_world4_gloo_matches_oracle(tmp_path):
