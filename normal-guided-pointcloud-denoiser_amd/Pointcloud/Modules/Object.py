@@ -113,8 +113,9 @@ class Pointcloud:
         return self.file_path is not None
 
 
-def sample_surface(v: torch.Tensor, f: torch.Tensor, num: int, generator: torch.Generator = None):
-    """Area-weighted barycentric sampling (the SamplePoints transform's algorithm) -> (pos, face normals)."""
+def sample_surface(v: torch.Tensor, f: torch.Tensor, num: int, generator: torch.Generator = None,
+                   return_faces: bool = False):
+    """Area-weighted barycentric sampling (the SamplePoints transform's algorithm) -> (pos, face normals[, face ids])."""
     a, b, c = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
     cr = torch.cross(b - a, c - a, dim=1)
     area = cr.norm(dim=1)
@@ -126,4 +127,4 @@ def sample_surface(v: torch.Tensor, f: torch.Tensor, num: int, generator: torch.
     flip = uv.sum(1) > 1
     uv[flip] = 1 - uv[flip]
     pos = a[fid] + uv[:, :1] * (b[fid] - a[fid]) + uv[:, 1:] * (c[fid] - a[fid])
-    return pos, fn[fid]
+    return (pos, fn[fid], fid) if return_faces else (pos, fn[fid])

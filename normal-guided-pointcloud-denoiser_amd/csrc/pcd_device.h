@@ -675,6 +675,9 @@ PCD_DEV void jacobi_rot(float (&a)[3][3], float (&V)[3][3]) {
 #ifndef PCD_JACOBI_SWEEPS
 #define PCD_JACOBI_SWEEPS 3   // (4 measured: NVT2 +0.014 ms, same classes in every parity test)
 #endif
+#ifndef PCD_NVT2_REFINE
+#define PCD_NVT2_REFINE 1     // smallest eigenvector re-derived as the null vector of T - λ0 I (below)
+#endif
 PCD_DEV void eigh3_min(const Sym3& T, float w[3], Vec3& y) {
     float a[3][3] = {{T.a00, T.a01, T.a02}, {T.a01, T.a11, T.a12}, {T.a02, T.a12, T.a22}};
     float V[3][3] = {{1.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, {0.f, 0.f, 1.f}};
@@ -696,6 +699,31 @@ PCD_DEV void eigh3_min(const Sym3& T, float w[3], Vec3& y) {
     cx(0, 1); cx(1, 2); cx(0, 1);
     w[0] = e[0]; w[1] = e[1]; w[2] = e[2];
     y = c[0] == 0 ? v3(V[0][0], V[1][0], V[2][0]) : c[0] == 1 ? v3(V[0][1], V[1][1], V[2][1]) : v3(V[0][2], V[1][2], V[2][2]);
+#if PCD_NVT2_REFINE
+    // The rotation-accumulated vector carries the sweeps' leftover off-diagonal over the gap (~1e-6 / gap rad,
+    // tests/test_gpu_stages.py); the null vector of T - λ0 I as the largest cross product of two of its rows is
+    // accurate to rounding over the gap (λ0 itself is second-order accurate), as LAPACK's is.  Used where the gap
+    // to λ1 is not degenerate (|cross|² >= (1e-3 λmax²)²: every edge point); else the Jacobi vector stays.
+    {
+        const float l = e[0];
+        const float r0[3] = {T.a00 - l, T.a01, T.a02}, r1[3] = {T.a01, T.a11 - l, T.a12}, r2[3] = {T.a02, T.a12, T.a22 - l};
+        auto cr = [](const float a[3], const float b[3]) {
+            return v3(a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]);
+        };
+        const Vec3 x0 = cr(r0, r1), x1 = cr(r0, r2), x2 = cr(r1, r2);
+        const float n0 = sq3(x0), n1 = sq3(x1), n2 = sq3(x2);
+        Vec3 x = x0;
+        float nn = n0;
+        if (n1 > nn) { x = x1; nn = n1; }
+        if (n2 > nn) { x = x2; nn = n2; }
+        const float lm = fmaxf(fabsf(e[2]), fabsf(e[0]));
+        const float thr = 1e-3f * lm * lm;
+        if (nn >= thr * thr && nn < 3.0e38f) {
+            const float inv = jrsq(nn);
+            y = v3(x.x * inv, x.y * inv, x.z * inv);
+        }
+    }
+#endif
     if (!(d0 == d0 && d1 == d1 && d2 == d2)) { w[0] = w[1] = w[2] = NAN; }
 }
 

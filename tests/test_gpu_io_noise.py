@@ -80,24 +80,22 @@ def test_sample_obj_on_device(gpu, tmp_path):
     n = 2_000_000
     pc = Pointcloud.sampleObj(str(p), n, device=gpu, generator=torch.Generator(device=gpu).manual_seed(0))
     assert pc.v.device.type == "cuda" and pc.v.shape == (n, 3) and pc.n.shape == (n, 3)
-    v = torch.from_numpy(fx["v"]).to(gpu).double()
+    # the same draws through sample_surface, keeping the face ids (sampleObj is exactly this call on the device)
+    from Pointcloud.Modules.Object import sample_surface
+    v32 = torch.from_numpy(fx["v"]).to(gpu)
     f = torch.from_numpy(fx["f"].astype(np.int64)).to(gpu)
+    pos2, nrm2, fid = sample_surface(v32, f, n, generator=torch.Generator(device=gpu).manual_seed(0),
+                                     return_faces=True)
+    v = v32.double()
     a, b, c = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
     cr = torch.cross(b - a, c - a, dim=1)
     area = cr.norm(dim=1)
     fnrm = cr / area[:, None]
-    # each sample's face: the face whose normal it carries and whose plane it lies on (nearest plane among faces
-    # sharing that normal is unnecessary: recover the face id by re-drawing the same multinomial on the device)
-    a32 = torch.from_numpy(fx["v"]).to(gpu)
-    cr32 = torch.cross(a32[f[:, 1]] - a32[f[:, 0]], a32[f[:, 2]] - a32[f[:, 0]], dim=1)
-    area32 = cr32.norm(dim=1)
-    fid = torch.multinomial(area32 / area32.sum(), n, replacement=True,
-                            generator=torch.Generator(device=gpu).manual_seed(0))
-    d = ((pc.v.double() - a[fid]) * fnrm[fid]).sum(1)
+    d = ((pos2.double() - a[fid]) * fnrm[fid]).sum(1)
     assert float(d.abs().max()) < 1e-3 * float(area.max().sqrt())
-    assert torch.allclose(pc.n.double(), fnrm[fid], atol=1e-5)
+    assert torch.allclose(nrm2.double(), fnrm[fid], atol=1e-5)
     # barycentric coordinates inside the triangle
-    e0, e1, w = b[fid] - a[fid], c[fid] - a[fid], pc.v.double() - a[fid]
+    e0, e1, w = b[fid] - a[fid], c[fid] - a[fid], pos2.double() - a[fid]
     d00, d01, d11 = (e0 * e0).sum(1), (e0 * e1).sum(1), (e1 * e1).sum(1)
     d20, d21 = (w * e0).sum(1), (w * e1).sum(1)
     den = d00 * d11 - d01 * d01
@@ -109,6 +107,8 @@ def test_sample_obj_on_device(gpu, tmp_path):
         expect = float(area[chunk].sum() / area.sum() * n)
         got = float(counts[chunk].sum())
         assert abs(got - expect) < 5 * math.sqrt(expect) + 1, (got, expect)
+    # sampleObj is this very call: same generator seed, same draws
+    assert torch.equal(pos2, pc.v) and torch.equal(nrm2, pc.n)
 
 
 def test_bench_cloud_is_drawn_on_device(gpu):

@@ -41,10 +41,11 @@ def angle(a, b):
     return np.arctan2(s, c)
 
 
-def staged_iteration(pos0, n0, d, dev, k=K, ku=KU, inject_fn=None):
+def staged_iteration(pos0, n0, d, dev, k=K, ku=KU, inject_fn=None, inject_pos=None):
     """One fused iteration driven stage by stage; returns the per-stage outputs in caller order.
-    inject_fn: the reference's smoothed normals, written over K1's f_n before NVT2 (pcd_denoiser_unpack FIELD_FN) so
-    that NVT2 and the phases are fed IDENTICAL inputs (SURVEY §8(c)'s single-step gates)."""
+    inject_fn: the reference's smoothed normals, written over K1's f_n before NVT2 (pcd_denoiser_unpack FIELD_FN);
+    inject_pos: the reference's positions after phases 0 and 1, written over the current positions before phases 1
+    and 2 -- so that NVT2 and every phase are fed IDENTICAL inputs (SURVEY §8(c)'s single-step gates)."""
     pos_t = torch.as_tensor(np.ascontiguousarray(pos0)).to(dev)
     n_t = torch.as_tensor(np.ascontiguousarray(n0)).to(dev)
     grid = nat.Grid(pos_t, k_hint=k)
@@ -64,7 +65,13 @@ def staged_iteration(pos0, n0, d, dev, k=K, ku=KU, inject_fn=None):
         fd.unpack(nat.FIELD_FN, torch.arange(N, device=dev, dtype=torch.int32), f4)
     fd.stage(p, nat.STAGE_NVT2)
     out["eig2"] = fd.probe().cpu().numpy()
+    rows_all = torch.arange(N, device=dev, dtype=torch.int32)
+    perm = grid.perm().long()                           # spatial row -> caller index
     for ph in range(3):
+        if inject_pos is not None and ph > 0:
+            q4 = torch.zeros((N, 4), dtype=torch.float32, device=dev)
+            q4[:, :3] = torch.as_tensor(np.ascontiguousarray(inject_pos[ph - 1])).to(dev)[perm]
+            fd.unpack(nat.FIELD_POS, rows_all, q4)
         if p.phase_kind[ph] in (nat.STEP_FLAT, nat.STEP_NEW):
             fd.stage(p, nat.STAGE_PHASE_SUM, ph, red4)
             fd.stage(p, nat.STAGE_PHASE_CENTRE, ph, red4)
@@ -124,12 +131,20 @@ def check_stages(got, ref_cls, ref_fn, ref_eig2, ref_edge, ref_after, knn, pos0,
         dev_ = np.linalg.norm(got[f"pos_after_{ph}"] - ref_after[ph], axis=1) / bbox
         moved = ref_cls == ph
         m = dec_ok & moved
-        stats[ph] = (float(dev_[m].max()), float(np.percentile(dev_[m], 99.9)), float(1 - dec_ok[moved].mean()))
-        assert np.percentile(dev_[m], 99.9) <= 1e-6, (label, ph, stats[ph])
+        stats[ph] = (float(dev_[m].max()), float(np.percentile(dev_[m], 99)), float(np.percentile(dev_[m], 99.9)),
+                     float(1 - dec_ok[moved].mean()))
+        # The flat step returns v + di (rounding relative to the small move): 1e-6 x bbox at p99.9.
+        # The edge and feature steps return the solution x of a 3x3 system in ABSOLUTE coordinates, so fp32 rounding
+        # scales with |x| cond(A) eps -- the reference inverts A (inv_ex, then A^-1 b), the kernels solve by LU:
+        # p99 <= 2e-6, p99.9 <= 3e-6 x bbox.  Measured: the library built with NVT2 on the LAPACK
+        # ssyevd restatement (PCD_NVT2_LAPACK) shows the same 1.4-2.2e-6 at p99.9 in the edge phase as the shipped
+        # Jacobi, with every phase fed the reference's own inputs -- the steps' conditioning, not the solver.
+        assert np.percentile(dev_[m], 99.9) <= (1e-6 if ph == 0 else 3e-6), (label, ph, stats[ph])
+        assert np.percentile(dev_[m], 99) <= (1e-6 if ph == 0 else 2e-6), (label, ph, stats[ph])
         if ph == 0:
             assert (dev_[dec_ok & ~moved] == 0).all(), (label, ph)   # the flat phase copies the others
     assert dec_ok.mean() > (0.99 if injected else 0.90), (label, dec_ok.mean())
-    print(label, "excluded", round(float(excl), 5), "eig max", float(e.max()), "phases (max, p99.9, excluded)", stats)
+    print(label, "excluded", round(float(excl), 5), "eig max", float(e.max()), "phases (max, p99, p99.9, excluded)", stats)
     return stats
 
 
@@ -137,10 +152,11 @@ def check_stages(got, ref_cls, ref_fn, ref_eig2, ref_edge, ref_after, knn, pos0,
 def test_fused_stages_match_reference_fixture(golden, gpu, injected):
     """fandisk_k32 (the reference's own run, make_golden.py): one fused iteration, stage by stage."""
     f = golden("fandisk_k32")
-    got = staged_iteration(f["pos0"], f["n0"], float(f["d"]), gpu, inject_fn=f["it1_f_n"] if injected else None)
+    ref_after = [f["it1_pos_after_0"], f["it1_pos_after_1"], f["it1_pos_after_2"]]
+    got = staged_iteration(f["pos0"], f["n0"], float(f["d"]), gpu, inject_fn=f["it1_f_n"] if injected else None,
+                           inject_pos=ref_after if injected else None)
     # the kNN list the loop used IS the reference's (frozen snapshot, current = snapshot positions at iteration 1)
     assert (got["knn"][:, :K] == f["knn32"]).mean() > 0.999
-    ref_after = [f["it1_pos_after_0"], f["it1_pos_after_1"], f["it1_pos_after_2"]]
     check_stages(got, f["it1_classes"], f["it1_f_n"], f["it1_eigval2"], f["it1_eigvec2"][..., 0], ref_after,
                  f["knn32"], f["pos0"], "fandisk", injected)
 
@@ -156,9 +172,10 @@ def test_fused_stages_match_oracle_headline_sample(gpu, injected):
     d = 2 * O.mean_edge_length(p0, knn)
     rec = {}
     O.denoise_iteration(p0, n0, knn, d, K, KU, record=rec)
-    got = staged_iteration(p0, n0, d, gpu, inject_fn=rec["f_n"] if injected else None)
-    assert (got["knn"][:, :K] == rec["knn"]).mean() > 0.999
     ref_after = [rec["pos_after_0"], rec["pos_after_1"], rec["pos_after_2"]]
+    got = staged_iteration(p0, n0, d, gpu, inject_fn=rec["f_n"] if injected else None,
+                           inject_pos=ref_after if injected else None)
+    assert (got["knn"][:, :K] == rec["knn"]).mean() > 0.999
     check_stages(got, rec["classes"], rec["f_n"], rec["eigval2"], rec["edge_vectors"], ref_after, rec["knn"], p0,
                  "headline-200k", injected)
 
@@ -206,7 +223,12 @@ def test_nvt2_jacobi_matches_lapack_restatement(gpu):
     gap = (w0[:, 1] - w0[:, 0]) / np.maximum(lmax, 1e-30)
     ok = gap > 1e-4
     a = angle(y1[ok], V0[ok][..., 0])
-    bound = 2e-6 / gap[ok] + 2e-6                     # ~16 ulps of rotation per unit relative gap
+    ag = a * gap[ok]
+    print("eigh3_min vector error x gap: p50 %.3g p99 %.3g max %.3g; angle max %.3g" %
+          (np.median(ag), np.percentile(ag, 99), ag.max(), a.max()))
+    # the refined vector (null vector of T - λ0 I, PCD_NVT2_REFINE) is within ~4 ulps per unit relative gap of LAPACK's
+    # (measured max 2.5e-7 / gap; the rotation-accumulated Jacobi vector alone: 3.2e-6 / gap)
+    bound = 5e-7 / gap[ok] + 5e-7
     assert (a <= bound).all(), (a / bound).max()
     assert np.allclose(np.linalg.norm(y1, axis=1), 1, atol=1e-5)
 
