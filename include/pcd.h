@@ -22,7 +22,8 @@
  *   pcd_step_csr                    Denoiser.{flat,edge,feature,corner,new,dummy}_step  Pointcloud/Modules/Denoiser.py:26-232
  *   pcd_edge_length_sum             TorchUtils.averageEdgeLength               Pointcloud/Modules/Utils.py:297-299
  *   pcd_nn_dist                     TorchUtils.Chamfer/Paper/HausdorffDistance Pointcloud/Modules/Utils.py:253-295
- *   pcd_mesh_update                 Mesh.updateVertices                        PatchGeneration/Modules/Mesh.py:377-418
+ *   pcd_mesh_update(_f32)           Mesh.updateVertices                        PatchGeneration/Modules/Mesh.py:377-418
+ *   pcd_mesh_vta                    igl.vertex_triangle_adjacency (Mesh.__init__) PatchGeneration/Modules/Mesh.py:26
  *   pcd_denoiser_*                  Processor.denoise / getMyFeatureDecomposition / denoiseUntilMinimumError loop body
  *                                                                              Pointcloud/Modules/Processor.py:110-185
  *   pcd_orient_normals_mst          GraphBuilder.flipNormals (MST + DFS, host) Pointcloud/Modules/GraphBuilder.py:129-209
@@ -152,6 +153,15 @@ int pcd_nn_dist(const pcd_grid* g, const float* q, int64_t nq, float* d2_out, in
  * f [nf][3] int64, fn [nf][3] f64, vf/ni = igl vertex_triangle_adjacency (VF [3nf], NI [nv+1]) int64. */
 int pcd_mesh_update(double* v, int64_t nv, const int64_t* f, const double* fn, int64_t nf, const int64_t* vf,
                     const int64_t* ni, int k, void* stream);
+/* The same k Jacobi sweeps in fp32 (v [nv][3] f32 in place, f [nf][3] int32, fn [nf][3] f32, vf / ni int32): vertex and
+ * normal rows as float4 and faces as int4 internally, one thread per vertex.  Not bitwise the fp64 path: within fp32
+ * rounding of it (tests/test_gpu_mesh.py). */
+int pcd_mesh_update_f32(float* v, int64_t nv, const int32_t* f, const float* fn, int64_t nf, const int32_t* vf,
+                        const int32_t* ni, int k, void* stream);
+/* igl.vertex_triangle_adjacency (the reference's Mesh.__init__, PatchGeneration/Modules/Mesh.py:26) on the device:
+ * f [nf][3] (int32 or int64 per f_bits) -> vf [3 nf] (the incident faces of each vertex in increasing face order) and
+ * ni [nv + 1] offsets, int32 or int64 per out_bits.  PCD_ERR_ARG for a face index outside [0, nv).  Synchronises. */
+int pcd_mesh_vta(const void* f, int f_bits, int64_t nf, int64_t nv, void* vf, void* ni, int out_bits, void* stream);
 
 /* ------------------------------------------------------------------ fused denoise loop (H8, H13, H14) */
 typedef struct pcd_denoiser pcd_denoiser;

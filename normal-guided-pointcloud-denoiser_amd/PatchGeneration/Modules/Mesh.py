@@ -4,8 +4,9 @@
     v_i += Σ_{f∋i} Σ_{c∈f} n_f (n_f · (v_c − v_i)) / (3 deg_i)
 in fp64 on the HIP device (pcd_mesh_update, one thread per vertex over the vertex->face CSR) and writes the result
 back into `self.v` in place, like the reference's `v += scaled_S`.
-The vertex-triangle adjacency is igl's format (VF = incident faces grouped by vertex in face order, NI = offsets)
-computed here without igl.
+The vertex-triangle adjacency is igl's format (VF = incident faces grouped by vertex in face order, NI = offsets),
+built on the device (pcd_mesh_vta: a stable radix sort of the corners by vertex) and kept there with the faces;
+`updateVertices(n, k, fp32=True)` runs the fp32 kernel (pcd_mesh_update_f32).
 """
 from __future__ import annotations
 
@@ -31,8 +32,9 @@ class Mesh:
         self.f = f
         self.noise_factor = noise_factor
         self.f2f = f2f
-        self.vta = vta if vta is not None else vertex_triangle_adjacency(f, len(v))
+        self.vta = vta            # igl (VF, NI); None: built on the device on first use (pcd_mesh_vta)
         self.gt = gt
+        self._topo = {}           # device copies of the faces and the adjacency, per precision (they never change)
 
     @classmethod
     def readFile(cls, file_path: str) -> "Mesh":
@@ -50,17 +52,37 @@ class Mesh:
         return cr / np.linalg.norm(cr, axis=1)[:, None]
 
     def getVertexTriangleAdjacency(self):
+        if self.vta is None:
+            vf, ni = self._topology(False)[1:]
+            self.vta = (vf.cpu().numpy(), ni.cpu().numpy())
         return self.vta
 
-    def updateVertices(self, n, k=15):
+    def _topology(self, fp32: bool):
+        """(faces, VF, NI) on the device, int32 for the fp32 path, int64 for fp64; the adjacency is the caller's vta
+        when one was given, else built on the device."""
+        key = (bool(fp32), id(self.f), np.shape(self.f))
+        if key not in self._topo:
+            it = torch.int32 if fp32 else torch.int64
+            fd = torch.as_tensor(np.ascontiguousarray(self.f)).to(_nat.device()).to(it).contiguous()
+            if self.vta is not None:
+                vf, ni = (torch.as_tensor(np.ascontiguousarray(a)).to(fd.device).to(it) for a in self.vta)
+            else:
+                vf, ni = _nat.mesh_vta(fd, len(self.v), out_dtype=it)
+            self._topo[key] = (fd, vf.contiguous(), ni.contiguous())
+        return self._topo[key]
+
+    def updateVertices(self, n, k=15, fp32: bool = False):
+        """Mesh.py:377-418: k Jacobi sweeps, in place on self.v.  fp32=True runs the fp32 kernel (float4 rows, int32
+        topology) instead of the reference's fp64 arithmetic."""
         v = self.getVertices()
-        vf, ni = self.getVertexTriangleAdjacency()
-        dev = _nat.device()
-        vd = torch.as_tensor(np.ascontiguousarray(v, dtype=np.float64)).to(dev)
-        fd = torch.as_tensor(np.ascontiguousarray(self.f, dtype=np.int64)).to(dev)
-        nd = torch.as_tensor(np.ascontiguousarray(n, dtype=np.float64)).to(dev)
-        vfd = torch.as_tensor(np.ascontiguousarray(vf, dtype=np.int64)).to(dev)
-        nid = torch.as_tensor(np.ascontiguousarray(ni, dtype=np.int64)).to(dev)
+        fd, vfd, nid = self._topology(fp32)
+        dev = fd.device
+        dt = torch.float32 if fp32 else torch.float64
+        vd = torch.as_tensor(np.ascontiguousarray(v)).to(dev).to(dt).contiguous()
+        nd = torch.as_tensor(np.ascontiguousarray(n)).to(dev).to(dt).contiguous()
         assert nd.shape == fd.shape, "one normal per face"
-        _nat.mesh_update(vd, fd, nd, vfd, nid, k)
+        if fp32:
+            _nat.mesh_update_f32(vd, fd, nd, vfd, nid, k)
+        else:
+            _nat.mesh_update(vd, fd, nd, vfd, nid, k)
         v[...] = vd.cpu().numpy().astype(v.dtype, copy=False)

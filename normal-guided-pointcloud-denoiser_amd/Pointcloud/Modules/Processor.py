@@ -131,6 +131,44 @@ class Processor:
             g.pos.copy_(pos_out.to(g.pos.dtype))
         g.n = n_out.to(device=g.pos.device, dtype=g.pos.dtype)
 
+    def cpsdDenoise(self, iterations: int = 50, d: float = None, alphas=(0.1, 1.0, 1.0), rho: float = 0.9,
+                    tau: float = 0.3, step_clamp_factor: float = 20000.0, k_update: int = 8):
+        """The CPSD ("Martin") comparison driver of the thesis results (PostProcessing.ipynb:1041-1062), on the device
+        op by op: per iteration getMartinFeatureDecomposition(r=d) (radius selection of the CURRENT positions against
+        the frozen snapshot, normal-filtered NVT, VU smoothing, normal-filtered PVT), VU classes (tau), kNN(k_update),
+        then flat_step / edge_step (PVT smallest eigenvector) / corner_step with alphas and the per-step clamp at
+        d * step_clamp_factor, all from the iteration's input positions (temp_pos = pos.clone()), and the GLOBAL clamp
+        against the positions at the start of the call (mask = ||temp_pos - original_pos|| < d).  graph.pos is updated
+        in place (masked), graph.n rebound to f_n.  d defaults to 2 x the mean kNN(6) edge length."""
+        g = self.graph
+        GeneralUtils.validateAttributes(g, ["pos", "n"])
+        if d is None:
+            d = 2 * float(self.meanEdgeLength())
+        d = float(d)
+        original_pos = g.pos.clone()
+        den = self.denoiser
+        for _ in range(iterations):
+            decomposition, f_n = self.getMartinFeatureDecomposition(r=d, rho=rho)
+            classes = decomposition.getVUFeatures(tau=tau)
+            selection = self.selector.getKNNSelection(k=k_update)
+            temp_pos = g.pos.clone()
+            for key in range(3):
+                indices = (classes == key).nonzero().flatten()
+                if indices.size(0) == 0:
+                    continue
+                sel = selection.filter(indices)
+                if key == 0:
+                    new_pos = den.flat_step(sel, f_n, d * step_clamp_factor, alphas[key])
+                elif key == 1:
+                    new_pos = den.edge_step(sel, f_n, decomposition.eigvec[..., 0], d * step_clamp_factor, alphas[key])
+                else:
+                    new_pos = den.corner_step(sel, f_n, d * step_clamp_factor, alphas[key])
+                temp_pos[indices] = new_pos.to(temp_pos.dtype)
+            mask = (temp_pos - original_pos).norm(dim=1) < d
+            with torch.no_grad():
+                g.pos[mask] = temp_pos[mask]
+            g.n = f_n
+
     def denoiseUntilMinimumError(self, gt_pos: torch.Tensor, strategy: dict, k: int = 7,
                                  alpha: list = [0.02, 0.02, 0.1], d: float = 200,
                                  error_funcs: list[Callable] = [TorchUtils.PaperDistance], N: int = 2 ** 4):

@@ -4,7 +4,7 @@
 // Per iteration:
 //   K1 knn_nvt1   kNN(k) of the current positions against the frozen snapshot, fused with the first tensor vote
 //                 (Decompositionor.getBetterFilteredNVT on n) and VU smoothing -> f_n; writes the kNN list
-//                 column-major [kcap][N] (coalesced per neighbour slot)
+//                 in 8-column row-major blocks (pcd_lists.h: whole 32-B sectors per row and block)
 //   K2 nvt2       second vote on f_n -> class (argmax of scaled features) + edge vector (smallest eigenvector)
 //   per phase (Gauss-Seidel across phases, Jacobi within, reference order flat -> edge -> corner):
 //     [flat/new]  rows_sum -> finish_centre -> rows_maxdist   (GLOBAL centre / delta, Denoiser.py:106-107)
@@ -23,6 +23,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include "pcd_knn.h"
+#include "pcd_lists.h"
 #include "pcd_ops.h"
 #include "pcd_qknn.h"
 
@@ -41,24 +42,23 @@ PCD_DEV T* at32(T* base, int64_t i) {
     return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (uint32_t)((uint32_t)i * (uint32_t)sizeof(T)));
 }
 
-struct ColNb {
+// Column t of row i of a stored list (blocked layout, pcd_lists.h), read from memory.
+PCD_DEV const int32_t* lelem(const int32_t* idx, int64_t n, int64_t i, int t) {
+    const char* b = reinterpret_cast<const char*>(idx + (int64_t)(t >> 3) * n * 8);
+    return reinterpret_cast<const int32_t*>(b + (uint32_t)((uint32_t)i * 32u + (uint32_t)(t & 7) * 4u));
+}
+struct BlkNb {
     const int32_t* idx;
     int64_t n, i;
-    PCD_DEV int64_t operator()(int t) const { return *at32(idx + (int64_t)t * n, i); }
+    PCD_DEV int64_t operator()(int t) const { return *lelem(idx, n, i, t); }
 };
-// Same, for a list read exactly once (NVT2): streamed past L2 so the neighbour gathers keep it.
-struct ColNbStream {
-    const int32_t* idx;
-    int64_t n, i;
-    PCD_DEV int64_t operator()(int t) const { return __builtin_nontemporal_load(at32(idx + (int64_t)t * n, i)); }
-};
-// A column-major list re-read from memory with out-of-range entries mapped to the row itself (the fallback pass
-// of nvt_tensor; an invalid entry is already reported by the kernel's own check).
-struct ColNbSafe {
+// A stored list re-read from memory with out-of-range entries mapped to the row itself (the fallback pass of
+// nvt_tensor; an invalid entry is already reported by the kernel's own check).
+struct BlkNbSafe {
     const int32_t* idx;
     int64_t n, i;
     PCD_DEV int64_t operator()(int t) const {
-        const int64_t j = *at32(idx + (int64_t)t * n, i);
+        const int64_t j = *lelem(idx, n, i, t);
         return (uint64_t)j < (uint64_t)n ? j : i;
     }
 };
@@ -159,7 +159,7 @@ struct Cover {
     }
 };
 
-// K1 epilogue (every kNN variant): store the list column-major, check it, NVT1 + eigh + VU smoothing -> f_n.
+// K1 epilogue (every kNN variant): store the list (blocked layout), check it, NVT1 + eigh + VU smoothing -> f_n.
 // dk = d² of the kstore-th neighbour.
 template <int K>
 PCD_DEV void k1_epilogue(const float4* __restrict__ pos, const float4* __restrict__ nrm, int64_t N, int64_t i,
@@ -168,19 +168,17 @@ PCD_DEV void k1_epilogue(const float4* __restrict__ pos, const float4* __restric
     bool bad = false;
 #pragma unroll
     for (int t = 0; t < K; ++t) {
-        if (t < kstore) {
-            // a list entry that is not a point would be an internal error: record it, never fault on it
-            if ((uint32_t)l[t] >= (uint32_t)N) { bad = true; l[t] = (int)i; }
-            __builtin_nontemporal_store(l[t], idx + (int64_t)t * N + i);   // streamed: keep L2 for the gathers
-        }
+        // a list entry that is not a point would be an internal error: record it, never fault on it
+        if (t < kstore && (uint32_t)l[t] >= (uint32_t)N) { bad = true; l[t] = (int)i; }
     }
+    store_list<K, true>(idx, N, i, kstore, l);   // streamed: keep L2 for the gathers
     if (bad) atomicOr(err, 1);
     if (!cov.holds(vi, dk)) atomicOr(err, 2);
 #ifdef PCD_EXP_NONVT
     const float4 n4 = nrm[i];
     __builtin_nontemporal_store(v4f{n4.x, n4.y, n4.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
 #else
-    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho, ColNbSafe{idx, N, i});
+    const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho, BlkNbSafe{idx, N, i});
     const float4 n4 = nrm[i];
     float w[3], V[3][3];
     eigh3(T, w, V);
@@ -210,9 +208,11 @@ __global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __re
     unsigned long long cap = kInfKey;
     if constexpr (SEED) {           // max key of last iteration's list >= this iteration's kstore-th key
         // all list rows first (K loads in flight), then their points; columns >= kstore re-read column 0
+        int sl[K];
+        load_list<K, true>(idx, N, i, kstore, sl);
         uint32_t sd[K];
 #pragma unroll
-        for (int t = 0; t < K; ++t) sd[t] = (uint32_t)__builtin_nontemporal_load(idx + (int64_t)(t < kstore ? t : 0) * N + i);
+        for (int t = 0; t < K; ++t) sd[t] = (uint32_t)(t < kstore ? sl[t] : sl[0]);
         cap = 0ull;
 #pragma unroll
         for (int t = 0; t < K; ++t) {
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __re
 
 // ------------------------------------------------------------------ anchored kNN (seeded iterations, K <= 32)
 // Every point keeps an ANCHOR: a position a it was searched at, the exact KA = 2K nearest snapshot points S of a
-// (alist, column-major [KA][N]) and D = the KA-th distance there (anc[i].w; < 0: none yet).  Every snapshot point
+// (alist, blocked [KA/8][N][8], pcd_lists.h) and D = the KA-th distance there (anc[i].w; < 0: none yet).  Every snapshot point
 // outside S is >= D from a, hence >= D - |q - a| from the current position q.  So when the kstore-th distance of q
 // over S is below D - |q - a| (with rounding margins), the kstore nearest of q over the WHOLE snapshot are the
 // kstore nearest over S, in the same (d², index) key order -- exact, with KA gathers and one sorting network
@@ -297,8 +297,12 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
             const float R = (a.w + delta) * (1.f + 1e-5f);
             const float S = 67108864.f / fmaxf(R * R, 1e-30f);
             uint32_t r[KA], c[KA];
+            {
+                int rl[KA];
+                load_list<KA, true>(alist, N, i, KA, rl);
 #pragma unroll
-            for (int t = 0; t < KA; ++t) r[t] = (uint32_t)__builtin_nontemporal_load(at32(alist + (int64_t)t * N, i));
+                for (int t = 0; t < KA; ++t) r[t] = (uint32_t)rl[t];
+            }
             int below = 0;
 #pragma unroll
             for (int t = 0; t < KA; ++t) {
@@ -319,11 +323,10 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
                 if (t < kstore) ok = ok && (c[t] >> 6) < (c[t + 1] >> 6);
             failed = !ok;
             if (ok) {
+                int out[K];
 #pragma unroll
-                for (int t = 0; t < K; ++t)
-                    if (t < kstore)
-                        __builtin_nontemporal_store((int32_t)s_r[(c[t] & 63u) * kAnchorBS + threadIdx.x],
-                                                    at32(idx + (int64_t)t * N, i));
+                for (int t = 0; t < K; ++t) out[t] = (int32_t)s_r[(c[t] & 63u) * kAnchorBS + threadIdx.x];
+                store_list<K, true>(idx, N, i, kstore, out);
             }
         }
     }
@@ -341,9 +344,10 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
     const Vec3 vi = v3(p4.x, p4.y, p4.z);
     int l[K];
     bool bad = false;
+    load_list<K>(idx, N, i, kstore, l);
 #pragma unroll
     for (int t = 0; t < K; ++t) {
-        l[t] = t < kstore ? *at32(idx + (int64_t)t * N, i) : (int)i;
+        l[t] = t < kstore ? l[t] : (int)i;
         if ((uint32_t)l[t] >= (uint32_t)N) { bad = true; l[t] = (int)i; }
     }
     if (bad) atomicOr(err, 1);
@@ -355,7 +359,7 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
         if (!cov.holds(vi, dk)) atomicOr(err, 2);
     }
     // 4 neighbours in flight per batch (8 measured 0.06 ms slower at 10M: the VGPRs of 8 rows in flight)
-    const Sym3 T = nvt_tensor<K, true, UNIT, 4>(rp, rn, vi, k, RegNb32{l}, rho, ColNbSafe{idx, N, i});
+    const Sym3 T = nvt_tensor<K, true, UNIT, 4>(rp, rn, vi, k, RegNb32{l}, rho, BlkNbSafe{idx, N, i});
     float w[3], V[3][3];
     eigh3(T, w, V);
     const float4 n4 = nrm[i];
@@ -441,7 +445,7 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
             const float4 a = anc[i];
             // (D + |q - a|)² bounds the KA-th key at q only for a FULL anchor set (KA points within D of a); a partial
             // set (fewer points within its radius, unused slots = N, the +inf sentinel row) gives no such bound
-            if (a.w >= 0.f && (uint32_t)alist[(int64_t)(KA - 1) * N + i] < (uint32_t)N) cap = anchor_cap(q, a);
+            if (a.w >= 0.f && (uint32_t)alist[lpos(N, i, KA - 1)] < (uint32_t)N) cap = anchor_cap(q, a);
         }
         const unsigned long long top = wave_knn<KA>(g, q, cap, s_buf[wv], &s_cells[wv], lane);
         // a slot without a finite candidate (non-finite query, fewer than KA points) is never stored as an index:
@@ -451,11 +455,11 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
         const int32_t r = valid ? (int32_t)r32 : (int32_t)i;
         const bool all_valid = !__any(lane < KA && !valid);
         if (!all_valid && lane == 0) atomicOr(err, 1);
-        if (lane < kstore) idx[(int64_t)lane * N + i] = r;
+        if (lane < kstore) idx[lpos(N, i, lane)] = r;   // (whole 32-B sectors, pcd_lists.h)
         {   // the anchor set in rank order (see k_knn_requery), unused slots last
             uint32_t v[1] = {lane < KA ? (uint32_t)r : 0xFFFFFFFFu};
             grp_bitonic_sort32<64, 1>(v, lane);
-            if (lane < KA) alist[(int64_t)lane * N + i] = (int32_t)v[0];
+            if (lane < KA) alist[lpos(N, i, lane)] = (int32_t)v[0];
         }
         // D: the KA-th distance (every other snapshot point is at least this far from the anchor)
         if (lane == KA - 1)
@@ -482,8 +486,10 @@ __global__ __launch_bounds__(kNvtBS) void k_nvt2(const float4* __restrict__ pos,
     // classes and the edge vector are invariant to the positive scale 1/Σw (ratios of eigenvalues, a unit
     // eigenvector): the tensor is left unnormalised.  f_n is NVT1's normalised output: the vote margin is constant.
     int wsum = 0;
+    int l[K];
+    load_list<K, true>(idx, N, i, k, l);   // read once: streamed past L2 so the neighbour gathers keep it
     const Sym3 T = nvt_tensor<K, PCD_NVT2_NORM, true>(WinRows<kWinHaloNvt2, kNvtBS>{pos, s_pos, lo}, WinRows<kWinHaloNvt2, kNvtBS>{fn, s_fn, lo},
-                                                v3(p4.x, p4.y, p4.z), k, ColNbStream{idx, N, i}, rho, ColNbSafe{idx, N, i},
+                                                v3(p4.x, p4.y, p4.z), k, RegNb32{l}, rho, BlkNbSafe{idx, N, i},
                                                 probe ? &wsum : nullptr);
 #ifdef PCD_NVT2_LAPACK
     float w[3], V[3][3];
@@ -510,9 +516,8 @@ struct RedC { double sx, sy, sz, cnt; };
 template <int KU>
 PCD_DEV void gather_rows(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N, int64_t i, int ku,
                          float4 (&v)[KU]) {
-    int32_t j[KU];
-#pragma unroll
-    for (int u = 0; u < KU; ++u) j[u] = idx[(int64_t)(u < ku ? u : ku - 1) * N + i];
+    int j[KU];
+    load_list_clamped<KU>(idx, N, i, ku, j);   // (block 0: two 16-B loads per lane)
 #pragma unroll
     for (int u = 0; u < KU; ++u) v[u] = pos[j[u]];
 }
@@ -652,11 +657,15 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     }
     const Vec3 vi = v3(p4.x, p4.y, p4.z);
     const Rows4 P{pin}, F{fn};
-    const ColNb nb{idx, N, i};
+    int l[KU];
+    // the update list: block 0 (pcd_lists.h), 16-B loads (8-B in the windowed flat phase: load_list_clamped8)
+    if constexpr (WIN) load_list_clamped8<KU>(idx, N, i, ku, l);
+    else load_list_clamped<KU>(idx, N, i, ku, l);
+    const RegNbC nb{l};
     Vec3 o;
     if constexpr (WIN)
-        o = step_flat<KU>(WinRows<kWinHaloPhase, 256>{pin, s_pos, lo}, WinRows<kWinHaloPhase, 256>{fn, s_fn, lo}, vi, F(i), ku, nb,
-                          __uint_as_float(((const unsigned*)g)[3]), d, alpha);
+        o = step_flat<KU>(WinRows<kWinHaloPhase, 256>{pin, s_pos, lo}, WinRows<kWinHaloPhase, 256>{fn, s_fn, lo}, vi, F(i), ku,
+                          nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
     else if (KIND == PCD_STEP_FLAT) o = step_flat<KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
     else if (KIND == PCD_STEP_EDGE) o = step_edge<KU, 4>(P, F, vi, Rows4{edge}(i), ku, nb, d, alpha);
     else if (KIND == PCD_STEP_FEATURE) o = step_feature<false, KU, 4>(P, F, vi, F(i), ku, nb, 1.f, d, alpha);
@@ -678,14 +687,14 @@ __global__ void k_scatter4(const float4* __restrict__ src, const int32_t* __rest
     if (r < N) out[perm[r]] = src[r];
 }
 
-// pcd_denoiser_lists: column-major sorted-order lists -> caller rows of original indices
+// pcd_denoiser_lists: blocked sorted-order lists -> caller rows of original indices
 __global__ void k_lists(const int32_t* __restrict__ idx, const int32_t* __restrict__ perm, int64_t N, int cols,
                         int64_t* __restrict__ out) {
     const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (r >= N) return;
     const int64_t i = perm[r];
     for (int t = 0; t < cols; ++t) {
-        const int32_t j = idx[(int64_t)t * N + r];
+        const int32_t j = idx[lpos(N, r, t)];
         out[i * cols + t] = (uint32_t)j < (uint64_t)N ? (int64_t)perm[j] : -1;
     }
 }
@@ -1043,8 +1052,9 @@ int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out) {
     *out = nullptr;
     PCD_CHECK_ARG(g != nullptr, "grid is null");
     PCD_CHECK_ARG(k_max >= 1 && k_max <= pcd_max_k(), "k_max out of range");
-    // the kernels address rows and list columns by 32-bit byte offsets from uniform bases (at32): 16 B x N < 4 GiB
-    PCD_CHECK_ARG(g->n < (1ll << 28), "more than 2^28 points per denoiser (split into spatial slabs)");
+    // the kernels address rows and list blocks by 32-bit byte offsets from uniform bases (at32, pcd_lists.h):
+    // 32 B x N < 4 GiB
+    PCD_CHECK_ARG(g->n < (1ll << 27), "more than 2^27 points per denoiser (split into spatial slabs)");
     pcd_denoiser* dn = new pcd_denoiser();
     dn->g = g;
     dn->n = g->n;
@@ -1056,7 +1066,7 @@ int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out) {
               hipMalloc(&dn->fn, N * sizeof(float4)) == hipSuccess &&
               hipMalloc(&dn->edge, N * sizeof(float4)) == hipSuccess &&
               hipMalloc(&dn->orig, N * sizeof(float4)) == hipSuccess &&
-              hipMalloc(&dn->idx, (int64_t)k_max * N * sizeof(int32_t)) == hipSuccess &&
+              hipMalloc(&dn->idx, (int64_t)knn_cap(k_max) * N * sizeof(int32_t)) == hipSuccess &&
               hipMalloc(&dn->cls, N) == hipSuccess &&
               hipMalloc(&dn->part, kNumPart * sizeof(RedC)) == hipSuccess &&
               hipMalloc(&dn->red, 16 * sizeof(double)) == hipSuccess &&

@@ -14,12 +14,16 @@ static constexpr int kNbBatch = PCD_NB_BATCH;   // neighbours gathered together 
 // Neighbour loop of a fused kernel: M = compile-time bound on cnt (list cap).  The list entries are read first, then
 // the neighbours' (v_j, n_j) in batches of kNbBatch whose loads are all issued before any is consumed; f(vj, nj) runs
 // for t < cnt in list order, so every sum keeps the reference's summation order.  M = 0: plain runtime loop.
+// A list accessor with `static constexpr bool kClamped = true` already repeats entry cnt-1 past cnt, so it is read at
+// compile-time slots (a register list needs no run-time index).
+template <class Nb, class = void> struct nb_clamped { static constexpr bool value = false; };
+template <class Nb> struct nb_clamped<Nb, decltype((void)Nb::kClamped)> { static constexpr bool value = Nb::kClamped; };
 template <int M, int BATCH = kNbBatch, class P, class Nr, class Nb, class F>
 PCD_DEV void for_neighbours(P pos, Nr nrm, int cnt, Nb nb, F&& f) {
     if constexpr (M > 0) {
         int32_t jj[M];
 #pragma unroll
-        for (int t = 0; t < M; ++t) jj[t] = (int32_t)nb(t < cnt ? t : cnt - 1);
+        for (int t = 0; t < M; ++t) jj[t] = (int32_t)(nb_clamped<Nb>::value ? nb(t) : nb(t < cnt ? t : cnt - 1));
 #pragma unroll
         for (int b = 0; b < M; b += BATCH) {
             constexpr int B = M < BATCH ? M : BATCH;

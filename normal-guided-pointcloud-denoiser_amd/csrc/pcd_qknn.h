@@ -15,6 +15,7 @@
 // DENSE (no anchors yet): the cap radius is r_scale · h · (16 / n)^(1/3), n = occupancy of the query's cell; a
 // query with fewer than KA points inside it is spilled (the wave search then grows its own box).
 #pragma once
+#include "pcd_lists.h"
 #include "pcd_wknn.h"
 
 namespace pcd {
@@ -450,8 +451,9 @@ PCD_DEV bool rq_query(const GridView& g, const Src& src, int64_t i, Vec3 q, floa
     const unsigned long long m1 = h1 ? buf[o.s1 & 255u] : 0ull;
     const int32_t r0 = h0 ? (int32_t)(uint32_t)(m0 & 0xFFFFFFFFull) : (int32_t)N;   // N: the +inf sentinel row
     const int32_t r1 = h1 ? (int32_t)(uint32_t)(m1 & 0xFFFFFFFFull) : (int32_t)N;
-    if (e0 < kstore) idx[(int64_t)e0 * N + i] = r0;
-    if (e1 < kstore) idx[(int64_t)e1 * N + i] = r1;
+    // whole 32-B sectors of the blocked list layout (pcd_lists.h): lanes 8b .. 8b+7 fill block b of row i
+    if (e0 < kstore) idx[lpos(N, i, e0)] = r0;
+    if (e1 < kstore) idx[lpos(N, i, e1)] = r1;
     // the anchor set is stored in RANK order (unused slots last): the anchor test ranks it by distance itself,
     // and neighbouring rows -- neighbouring lanes of its waves -- then gather nearly the same snapshot rows in the
     // same slot, i.e. the same cache lines, instead of 64 unrelated ones per gather instruction
@@ -461,8 +463,8 @@ PCD_DEV bool rq_query(const GridView& g, const Src& src, int64_t i, Vec3 q, floa
         v[0] = e0 < KA ? (uint32_t)r0 : 0xFFFFFFFFu;
         if (M > 1) v[M - 1] = e1 < KA ? (uint32_t)r1 : 0xFFFFFFFFu;
         grp_bitonic_sort32<W, M>(v, lg.hl);
-        if (e0 < KA) alist[(int64_t)e0 * N + i] = (int32_t)v[0];
-        if (M > 1 && e1 < KA) alist[(int64_t)e1 * N + i] = (int32_t)v[M - 1];
+        if (e0 < KA) alist[lpos(N, i, e0)] = (int32_t)v[0];
+        if (M > 1 && e1 < KA) alist[lpos(N, i, e1)] = (int32_t)v[M - 1];
     }
     // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
     // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))

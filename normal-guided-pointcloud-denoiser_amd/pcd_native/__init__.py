@@ -69,6 +69,9 @@ _SIGS = {
     "pcd_edge_length_sum": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "pcd_nn_dist": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "pcd_mesh_update": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
+    "pcd_mesh_update_f32": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int,
+                                    c_void_p]),
+    "pcd_mesh_vta": (c_int, [c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
     "pcd_denoiser_create": (c_int, [c_void_p, c_int, POINTER(c_void_p)]),
     "pcd_denoiser_destroy": (c_int, [c_void_p]),
     "pcd_denoiser_load": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -489,6 +492,26 @@ def edge_length_sum(pos, a, b):
 def mesh_update(v, f, fn, vf, ni, k):
     check(lib().pcd_mesh_update(ptr(v), v.size(0), ptr(f), ptr(fn), f.size(0), ptr(vf), ptr(ni), int(k),
                                 c_void_p(stream_ptr())), "pcd_mesh_update")
+
+
+def mesh_update_f32(v, f, fn, vf, ni, k):
+    """fp32 sweeps: v float32 [nv,3] (in place), f int32 [nf,3], fn float32 [nf,3], vf / ni int32 (device)."""
+    assert v.dtype == torch.float32 and fn.dtype == torch.float32
+    assert f.dtype == torch.int32 and vf.dtype == torch.int32 and ni.dtype == torch.int32
+    check(lib().pcd_mesh_update_f32(ptr(v), v.size(0), ptr(f), ptr(fn), f.size(0), ptr(vf), ptr(ni), int(k),
+                                    c_void_p(stream_ptr())), "pcd_mesh_update_f32")
+
+
+def mesh_vta(f: torch.Tensor, nv: int, out_dtype=torch.int64):
+    """igl.vertex_triangle_adjacency on the device: (vf [3 nf], ni [nv + 1]) in out_dtype (int32 / int64)."""
+    f = on_device(f)
+    assert f.dtype in (torch.int32, torch.int64) and f.dim() == 2 and f.size(1) == 3
+    nf = f.size(0)
+    vf = torch.empty(3 * nf, dtype=out_dtype, device=f.device)
+    ni = torch.empty(nv + 1, dtype=out_dtype, device=f.device)
+    check(lib().pcd_mesh_vta(ptr(f), 32 if f.dtype == torch.int32 else 64, nf, int(nv), ptr(vf), ptr(ni),
+                             32 if out_dtype == torch.int32 else 64, c_void_p(stream_ptr())), "pcd_mesh_vta")
+    return vf, ni
 
 
 def grid_params(xyz: torch.Tensor, k_hint: int = 16, cell: float = 0.0):

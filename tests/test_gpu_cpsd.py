@@ -137,3 +137,28 @@ def test_cpsd_corner_step(cpsd, proc):
     bbox = np.linalg.norm(cpsd["pos"].max(0) - cpsd["pos"].min(0))
     dev = np.linalg.norm(out.cpu().numpy() - cpsd["corner_pos"], axis=1) / bbox
     assert np.median(dev) < 1e-6 and np.percentile(dev, 99) < 1e-4, np.percentile(dev, [50, 99, 100])
+
+
+def test_cpsd_driver_matches_oracle(cpsd, gpu):
+    """The 50-iteration CPSD driver (PostProcessing.ipynb:1041-1062) as Processor.cpsdDenoise: its first two
+    iterations against the oracle's composition of the same operators (pcd_oracle.cpsd_iteration) on the fandisk
+    fixture -- one iteration at the single-iteration tolerances of test_gpu_parity (median 1e-6, p99 3e-4 x bbox),
+    the second within the loop's chaotic envelope; the global clamp holds."""
+    pos0, n0 = cpsd["pos"], cpsd["n"]
+    d = float(cpsd["d"])
+    bbox = float(np.linalg.norm(pos0.max(0) - pos0.min(0)))
+    knn = O.FrozenKNN(pos0)
+    rp, rn = pos0.copy(), n0.copy()
+    for it in (1, 2):
+        rp, rn = O.cpsd_iteration(pos0, rp, rn, pos0, knn, d)
+        v = T(pos0, gpu).clone()
+        proc = Processor(Pointcloud(v, T(n0, gpu).clone()))
+        proc.cpsdDenoise(iterations=it, d=d)                         # original_pos = the call's input, as the ipynb
+        dev = np.linalg.norm(v.cpu().numpy() - rp, axis=1) / bbox
+        if it == 1:
+            assert np.median(dev) < 1e-6 and np.percentile(dev, 99) < 3e-4, (np.median(dev), np.percentile(dev, 99))
+        else:
+            assert np.median(dev) < 1e-5 and np.percentile(dev, 99) < 5e-3, (np.median(dev), np.percentile(dev, 99))
+        assert proc.graph.pos is v                                   # updated in place
+        moved = np.linalg.norm(v.cpu().numpy() - pos0, axis=1)
+        assert moved.max() < d                                        # the global clamp (ipynb:1060-1061)
