@@ -85,9 +85,9 @@ def b_alg_iteration(k, ku):
 
 
 def b_alg_knn_nvt1(k):
-    """Fused kNN + NVT1 kernel: query xyz 12 + k winners' snapshot xyz 12k + list write 4k (kNN) + current
-    v_j, n_j 24k + own n 12 + f_n write 12 (NVT1, the list and own position come from registers)."""
-    return 12 + 12 * k + 4 * k + 24 * k + 12 + 12
+    """K1 stage (kNN + NVT1), SURVEY.md §8(d): kNN 12 (query) + 12k (winners' xyz) + 4k (list write) and NVT1 4k (list)
+    + 12 (own v) + 24k (v_j, n_j) + 12 (own n) + 12 (f_n write) = 48 + 44k (1,456 B at k = 32)."""
+    return (12 + 12 * k + 4 * k) + (4 * k + 12 + 24 * k + 12 + 12)
 
 
 def make_cloud(n, seed, dev, sigma_frac=0.005, clean=False):
@@ -144,6 +144,101 @@ def cpu_baseline(k, ku, sample_points, dev, seed=99):
     return base, parity
 
 
+def mesh_bench(dev, cpu):
+    """Mesh.updateVertices (H18, PatchGeneration/Modules/Mesh.py:377-418): per-sweep time of the fp64 kernel (the
+    reference's arithmetic) and the fp32 kernel on the bunny mesh (the reference publishes 0.591 s/iteration for
+    Algorithm 3 on an unshipped mesh, Vertex_updating.ipynb:300) and on a 2048 x 2048 height-field grid (4.2M vertices)
+    for the fp32 roofline at 32 + 64 deg B/vertex; adjacency built on the device.  Per-sweep = (t(16
+    sweeps) - t(1 sweep)) / 15 by host wall clock around synchronised calls (excludes the fp32 path's row repacking)."""
+    m = np.load(os.path.join(ROOT, "data", "stanford_bunny_mesh.npz"))
+    out = {"reference_s_per_iteration": 0.591, "reference_source": "Vertex_updating.ipynb:300 (Algorithm 3 = "
+           "Mesh.updateVertices, author's CPU, mesh example_object.obj not shipped)"}
+
+    def per_sweep(v, f, fn, vf, ni, fp32):
+        fun = nat.mesh_update_f32 if fp32 else nat.mesh_update
+        ts = {}
+        for k in (1, 16):
+            best = float("inf")
+            for _ in range(3):
+                w = v.clone()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                fun(w, f, fn, vf, ni, k)
+                torch.cuda.synchronize()
+                best = min(best, time.perf_counter() - t0)
+            ts[k] = best
+        return (ts[16] - ts[1]) / 15
+
+    def setup(v, f, fp32):
+        it, ft = (torch.int32, torch.float32) if fp32 else (torch.int64, torch.float64)
+        vd = v.to(dev, ft).contiguous()
+        fd = f.to(dev, it).contiguous()
+        a, b, c = vd[fd[:, 0].long()], vd[fd[:, 1].long()], vd[fd[:, 2].long()]
+        cr = torch.cross(b - a, c - b, dim=1)
+        fn = (cr / cr.norm(dim=1, keepdim=True).clamp(min=1e-30)).contiguous()
+        vf, ni = nat.mesh_vta(fd, vd.size(0), out_dtype=it)
+        return vd, fd, fn, vf, ni
+
+    bv, bf = torch.from_numpy(m["v"].astype(np.float64)), torch.from_numpy(m["f"].astype(np.int64))
+    out["bunny"] = {"vertices": int(bv.size(0)), "faces": int(bf.size(0)),
+                    "fp64_ms_per_iteration": round(per_sweep(*setup(bv, bf, False), False) * 1e3, 4),
+                    "fp32_ms_per_iteration": round(per_sweep(*setup(bv, bf, True), True) * 1e3, 4)}
+    # a 2048 x 2048 grid mesh (two triangles per quad) over a smooth height field, on the device
+    n = 2048
+    ys, xs = torch.meshgrid(torch.linspace(0, 1, n, device=dev), torch.linspace(0, 1, n, device=dev), indexing="ij")
+    gv = torch.stack([xs, ys, 0.05 * torch.sin(12 * xs) * torch.cos(9 * ys)], -1).reshape(-1, 3)
+    q = torch.arange((n - 1) * (n - 1), device=dev)
+    r0 = (q // (n - 1)) * n + q % (n - 1)
+    gf = torch.cat([torch.stack([r0, r0 + 1, r0 + n], 1), torch.stack([r0 + 1, r0 + n + 1, r0 + n], 1)])
+    vd, fd, fn, vf, ni = setup(gv, gf, True)
+    t = per_sweep(vd, fd, fn, vf, ni, True)
+    nv, nf = vd.size(0), fd.size(0)
+    deg = 3 * nf / nv
+    alg = (32 + 64 * deg) * nv
+    out["grid_fp32"] = {"vertices": int(nv), "faces": int(nf), "ms_per_iteration": round(t * 1e3, 4),
+                        "roofline": {"bound": "hbm", "alg_bytes_per_vertex": round(32 + 64 * deg, 1),
+                                     "achieved": round(alg / t / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+                                     "note": "gather model: each incident face's normal, corners and corner rows "
+                                             "counted per use (L2 serves the re-reads)"}}
+    if cpu:
+        from oracle import pcd_oracle as O
+        vn, fn_ = m["v"].astype(np.float64), m["f"].astype(np.int64)
+        cr = np.cross(vn[fn_[:, 1]] - vn[fn_[:, 0]], vn[fn_[:, 2]] - vn[fn_[:, 1]])
+        nrm = cr / np.maximum(np.linalg.norm(cr, axis=1, keepdims=True), 1e-30)
+        t0 = time.perf_counter()
+        O.mesh_update(vn, fn_, nrm, k=3)
+        out["bunny"]["cpu_oracle_s_per_iteration"] = round((time.perf_counter() - t0) / 3, 4)
+    return out
+
+
+def cpsd_bench(dev, cpu, points=50_000, iterations=50):
+    """The CPSD ("Martin") 50-iteration driver (PostProcessing.ipynb:1041-1062, Processor.cpsdDenoise) on a 50k-point
+    bunny-sampled cloud: seconds per iteration against the reference's 1.13 s/it on the 50k-point Stitch_guitar
+    (PostProcessing.ipynb:1015, author's CPU)."""
+    pos, nrm, _ = make_cloud(points, 4, dev)
+    proc = Processor(Pointcloud(pos.clone(), nrm.clone()), k_hint=16)
+    d = 2 * float(proc.meanEdgeLength())
+    proc.cpsdDenoise(iterations=1, d=d)                  # warm-up (allocations, kernels)
+    proc = Processor(Pointcloud(pos.clone(), nrm.clone()), k_hint=16)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    proc.cpsdDenoise(iterations=iterations, d=d)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iterations
+    out = {"points": points, "iterations": iterations, "s_per_iteration": round(dt, 6),
+           "reference_s_per_iteration": 1.13, "reference_source": "PostProcessing.ipynb:1015 (50k-point Stitch_guitar, "
+           "author's CPU)", "speedup_vs_reference": round(1.13 / dt, 1)}
+    if cpu:
+        from oracle import pcd_oracle as O
+        p0, n0 = pos.cpu().numpy(), nrm.cpu().numpy()
+        knn = O.FrozenKNN(p0)
+        t0 = time.perf_counter()
+        O.cpsd_iteration(p0, p0, n0, p0, knn, d)
+        out["cpu_oracle_s_per_iteration"] = round(time.perf_counter() - t0, 4)
+    return out
+
+
 def measured_traffic(points, k, ms_per_step):
     """HBM bytes per iteration from profiles/traffic.json (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch, the
     gfx950 correction of MI355X_MICROARCH.md), summed over the iteration's kernels, against 8 TB/s."""
@@ -183,6 +278,10 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="N > 1 slabs: one global cloud of --points in total (strong scaling, BASELINE configs[4] "
                          "asks for 80M), instead of --points per GPU")
+    ap.add_argument("--long-run", type=int, default=100,
+                    help="continue the ten-iteration cloud to this iteration, per-iteration times (long_run)")
+    ap.add_argument("--no-extras", dest="extras", action="store_false",
+                    help="skip the mesh-update and CPSD-driver measurements (mesh_update, cpsd)")
     ap.add_argument("--no-rebalance", dest="rebalance", action="store_false",
                     help="slab mode: keep the equal-count cut (default: re-cut by class cost after warm-up 2)")
     ap.add_argument("--no-ten", dest="ten", action="store_false",
@@ -304,6 +403,7 @@ def main():
         torch.cuda.synchronize()
         ten_ms = (time.perf_counter() - t10) * 1e3
         fused.check()
+    long_run = None
     chamfer = None
     if mode != "slab" and args.ten:
         # the Chamfer distance of the 10-iteration result to the clean surface samples, at full size on the GPU
@@ -318,6 +418,23 @@ def main():
         cd_ms = (time.perf_counter() - tc) * 1e3
         cd_in = float(TorchUtils.ChamferDistance(surf, pos).mean())
         chamfer = {"points": args.points, "ms": round(cd_ms, 3), "cd_noisy": cd_in, "cd_10_iterations": cd_den}
+        # the long run (north_star: "iterated to convergence"): the same cloud on to iteration 100, per-iteration
+        # HIP-event time and re-anchored rows (the re-anchoring rate peaks near iteration 30)
+        fused.set_timing(True)
+        per_it, redo = {}, {}
+        for it in range(11, args.long_run + 1):
+            fused.iterate(params, 1)
+            per_it[it] = float(sum(fused.timing()))
+            redo[it] = fused.redo_rows()
+        fused.set_timing(False)
+        fused.check()
+        if per_it:
+            at = [a for a in (25, 50, 75, 100) if a in per_it]
+            long_run = {"iterations": args.long_run, "ms_at": {a: round(per_it[a], 4) for a in at},
+                        "redo_pct_at": {a: round(100 * redo[a] / args.points, 3) for a in at},
+                        "max_ms": round(max(per_it.values()), 4),
+                        "max_at": max(per_it, key=per_it.get),
+                        "mean_ms_last_20": round(float(np.mean([per_it[a] for a in sorted(per_it)[-20:]])), 4)}
 
     k1_points = sd.owned_global.numel() if mode == "slab" else args.points
     k1_bytes = b_alg_knn_nvt1(args.k) * k1_points
@@ -359,6 +476,8 @@ def main():
         "iterations_per_sec": round(1e3 / ms_per_step, 2),
         "first_iteration_ms": round(first_ms, 3) if first_ms is not None else None,
         "ten_iteration_ms": round(ten_ms, 3) if ten_ms is not None else None,
+        "iter_ms_at_100": long_run["ms_at"].get(100) if long_run else None,
+        "long_run": long_run,
         "chamfer": chamfer,
         "kernel_ms": kernel_ms,
         "stage_bound": STAGE_BOUND if mode != "slab" else None,
@@ -372,6 +491,9 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                      "traffic": traffic, "alg_bytes_per_launch": k1_bytes, "avg_launch_ms": round(knn_ms, 4)},
     }
+    if rank == 0 and world == 1 and args.extras:
+        out["mesh_update"] = mesh_bench(dev, not args.no_cpu_baseline)
+        out["cpsd"] = cpsd_bench(dev, not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["parity"] = cpu_baseline(args.k, args.k_update, args.cpu_sample, dev)
     if rank == 0:

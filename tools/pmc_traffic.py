@@ -4,6 +4,13 @@ HBM bytes per launch of each kernel = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: the 
 FETCH_SIZE tallies half the bytes of 16-B-per-lane reads (MI355X_MICROARCH.md, HBM / rocprofv3 section).  The raw
 values are kept next to the corrected ones.
 
+Calibrated per access width on the box (tools/calib_traffic.hip -> profiles/r3/calib_traffic.json): the x2 holds for
+coalesced 4-, 8- and 16-B/lane reads alike, and a random 16-B row gather counts 128 B (the missed line) after it;
+WRITE_SIZE is exact for coalesced stores and counts a 32-B sector per partial store.  So one factor serves every
+kernel here -- but FETCH_SIZE counts the L2's memory-side requests INCLUDING Infinity-Cache hits: a kernel whose
+gathered rows sit in the 256 MiB cache (k_edge_len's 160 MB of positions) can read "more than HBM bandwidth".  The
+bytes are L2-miss traffic, an upper bound on HBM traffic.
+
 usage: python tools/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> <points> <k> [out.json]
 """
 import csv
@@ -65,7 +72,9 @@ def main():
                 if e.get("hbm_bytes_per_launch") is not None:
                     per_iter += e["hbm_bytes_per_launch"] * e["launches_fetch"] / n_iter
     res = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, csv; "
-                     "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch (gfx950 FETCH_SIZE counts half)",
+                     "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch (gfx950 FETCH_SIZE counts half; x2 "
+                     "calibrated for 4/8/16-B reads and 16-B gathers, profiles/r3/calib_traffic.json); L2-miss bytes "
+                     "including Infinity-Cache hits (an upper bound on HBM bytes)",
            "points": points, "k": k, "iterations": n_iter, "per_iteration_bytes": per_iter,
            "source": os.path.relpath(fetch_csv), "kernels": kernels}
     with open(out, "w") as fh:
