@@ -490,7 +490,7 @@ __global__ __launch_bounds__(kNvtBS) void k_nvt2(const float4* __restrict__ pos,
     load_list<K, true>(idx, N, i, k, l);   // read once: streamed past L2 so the neighbour gathers keep it
     const Sym3 T = nvt_tensor<K, PCD_NVT2_NORM, true>(WinRows<kWinHaloNvt2, kNvtBS>{pos, s_pos, lo}, WinRows<kWinHaloNvt2, kNvtBS>{fn, s_fn, lo},
                                                 v3(p4.x, p4.y, p4.z), k, RegNb32{l}, rho, BlkNbSafe{idx, N, i},
-                                                probe ? &wsum : nullptr);
+                                                &wsum);   // (unconditional: a selected pointer would keep wsum in scratch)
 #ifdef PCD_NVT2_LAPACK
     float w[3], V[3][3];
     eigh3(T, w, V);
@@ -657,11 +657,10 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     }
     const Vec3 vi = v3(p4.x, p4.y, p4.z);
     const Rows4 P{pin}, F{fn};
-    int l[KU];
     // the update list: block 0 (pcd_lists.h), 16-B loads (8-B in the windowed flat phase: load_list_clamped8)
-    if constexpr (WIN) load_list_clamped8<KU>(idx, N, i, ku, l);
-    else load_list_clamped<KU>(idx, N, i, ku, l);
-    const RegNbC nb{l};
+    RegNbC<KU> nb;
+    if constexpr (WIN) load_list_clamped8<KU>(idx, N, i, ku, nb.l);
+    else load_list_clamped<KU>(idx, N, i, ku, nb.l);
     Vec3 o;
     if constexpr (WIN)
         o = step_flat<KU>(WinRows<kWinHaloPhase, 256>{pin, s_pos, lo}, WinRows<kWinHaloPhase, 256>{fn, s_fn, lo}, vi, F(i), ku,
@@ -675,7 +674,7 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     if (clampg > 0.f) {                 // global clamp against the loaded positions (PostProcessing.ipynb:1088-1089)
         const float4 o4 = orig[i];
         const bool keep = sqrtf(sq3(o - v3(o4.x, o4.y, o4.z))) < clampg;
-        o = keep ? o : vi;
+        o = sel3(keep, o, vi);
     }
     store4(pout, i, o);
 }

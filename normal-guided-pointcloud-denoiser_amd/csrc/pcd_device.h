@@ -26,6 +26,8 @@ PCD_DEV Vec3 operator*(float s, Vec3 a) { return v3(s * a.x, s * a.y, s * a.z); 
 // dot in the reference's summation order: (x*x' + y*y') + z*z'  ((a*b).sum(dim=1))
 PCD_DEV float dot3(Vec3 a, Vec3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }  // built with -ffp-contract=off
 PCD_DEV float sq3(Vec3 a) { return dot3(a, a); }
+// c ? a : b component by component (a select of the structs themselves can leave them in scratch memory)
+PCD_DEV Vec3 sel3(bool c, Vec3 a, Vec3 b) { return v3(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
 
 // ---------------------------------------------------------------- point accessors
 // Packed caller rows: float[n*3]

@@ -47,18 +47,22 @@ PCD_DEV void load_list(const int32_t* base, int64_t N, int64_t i, int cnt, int (
         }
     }
 }
-// A register list read at compile-time slots: entries past cnt repeat entry cnt - 1 (for_neighbours).
+// A register list read at compile-time slots: entries past cnt repeat entry cnt - 1 (for_neighbours).  Held BY VALUE:
+// a pointer to a local array keeps it in scratch memory.
+template <int M>
 struct RegNbC {
-    const int* l;
+    int l[M];
     static constexpr bool kClamped = true;
     PCD_DEV int64_t operator()(int t) const { return l[t]; }
 };
-// Row i's first M columns (cnt of them valid) into l, entries past cnt repeating entry cnt - 1.
+// Row i's first M columns (cnt of them valid, 1 <= cnt <= M) into l; entries past cnt repeat entry 0 (a valid row:
+// for_neighbours gathers them and drops the result).  Selects against a constant slot only: a chain (l[t - 1]) is
+// turned by the compiler into an indexed scratch access.
 template <int M, bool NT = false>
 PCD_DEV void load_list_clamped(const int32_t* base, int64_t N, int64_t i, int cnt, int (&l)[M]) {
     load_list<M, NT>(base, N, i, cnt, l);
 #pragma unroll
-    for (int t = 1; t < M; ++t) l[t] = t < cnt ? l[t] : l[t - 1];
+    for (int t = 1; t < M; ++t) l[t] = t < cnt ? l[t] : l[0];
 }
 
 // load_list_clamped with 8-B loads (the windowed flat phase: 16-B loads there trip an LLVM gfx950 backend error,
@@ -68,14 +72,14 @@ PCD_DEV void load_list_clamped8(const int32_t* base, int64_t N, int64_t i, int c
     typedef int v2i __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int q = 0; q < M / 2; ++q) {
-        if (2 * q < cnt || q == 0) {
+        if (8 * (q >> 2) < cnt) {                     // whole blocks (every block of a stored row is valid memory)
             const v2i x = *(reinterpret_cast<const v2i*>(lblock(base, N, i, q >> 2)) + (q & 3));
             l[2 * q] = x.x;
             l[2 * q + 1] = x.y;
         }
     }
 #pragma unroll
-    for (int t = 1; t < M; ++t) l[t] = t < cnt ? l[t] : l[t - 1];
+    for (int t = 1; t < M; ++t) l[t] = t < cnt ? l[t] : l[0];
 }
 
 // Store l[0 .. ceil(cnt / 8) * 8) as row i's first blocks (entries past cnt inside the last block are whatever l holds:

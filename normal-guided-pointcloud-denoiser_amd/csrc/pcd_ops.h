@@ -110,7 +110,7 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF n
             w = acosf(c) > rho;
         }
 #endif
-        const Vec3 nw = w ? nj : v3(0.f, 0.f, 0.f);
+        const Vec3 nw = sel3(w, nj, v3(0.f, 0.f, 0.f));
         acc0 += f2{nw.x, nw.x} * f2{nj.x, nj.y};
         acc1 += f2{nw.x, nw.y} * f2{nj.z, nj.y};
         acc2 += f2{nw.y, nw.z} * f2{nj.z, nj.z};
@@ -244,7 +244,7 @@ PCD_DEV void add_outer(float A[3][3], Vec3 a, float s = 1.f) {
 PCD_DEV Vec3 clamp_step(Vec3 vi, Vec3 x, float alpha, float d) {
     const Vec3 di = v3((x.x - vi.x) * alpha, (x.y - vi.y) * alpha, (x.z - vi.z) * alpha);
     const float nrm = sqrtf(sq3(di));
-    return (nrm < d) ? vi + di : vi;
+    return sel3(nrm < d, vi + di, vi);
 }
 
 // ----------------------------------------------------------------- H9: Denoiser.flat_step (Denoiser.py:90-119)
@@ -264,7 +264,7 @@ PCD_DEV Vec3 step_flat(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float de
     });
     const Vec3 di = v3(sx / ws * alpha, sy / ws * alpha, sz / ws * alpha);
     const float nrm2 = sqrtf(sq3(di));
-    return (nrm2 <= d) ? vi + di : vi;   // NaN (Σ W = 0) -> no move, as di[~mask] = 0
+    return sel3(nrm2 <= d, vi + di, vi);   // NaN (Σ W = 0) -> no move, as di[~mask] = 0
 }
 
 // ----------------------------------------------------------------- H10: Denoiser.edge_step (Denoiser.py:53-88)
