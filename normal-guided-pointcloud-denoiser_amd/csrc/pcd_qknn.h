@@ -82,8 +82,12 @@ PCD_DEV void grp_bitonic_sort32(uint32_t (&v)[M], int hl) {
     }
 }
 
-// Survivors per group: room for a cut to KA = 64 plus one round of appends (W * kRqRows).
-template <int W> struct RqSurv { static constexpr int n = W == 64 ? 256 : 192; };
+#ifndef PCD_RQ_ROWS
+#define PCD_RQ_ROWS 2
+#endif
+static constexpr int kRqRows = PCD_RQ_ROWS;   // candidate rows per lane per round (all loads in flight)
+// Survivors per group: room for 2W (W = 64; 4W at W = 32) before a cut plus one round of appends (W * kRqRows).
+template <int W> struct RqSurv { static constexpr int n = W == 64 ? 64 * (2 + kRqRows) : 32 * (4 + kRqRows); };
 
 // The quantised order of the survivors buf[0..cnt) (cnt <= RqSurv): element e lives in slot e / W of lane e % W;
 // o.s0 / o.s1 = this lane's elements hl and W + hl (0xFFFFFFFF past cnt), o.at(e) broadcasts element e.
@@ -227,10 +231,6 @@ PCD_DEV bool rq_cut(unsigned long long* buf, int& cnt, unsigned long long& cap, 
 // in 32-bit cell arithmetic, with the quantised buffer cut, for one lane group.  Returns false when a cut was
 // ambiguous (spill).
 static constexpr int kRqMaxCells = 4096;
-#ifndef PCD_RQ_ROWS
-#define PCD_RQ_ROWS 2
-#endif
-static constexpr int kRqRows = PCD_RQ_ROWS;   // candidate rows per lane per round (all loads in flight)
 #ifndef PCD_RQ_CELLS
 #define PCD_RQ_CELLS 64
 #endif
