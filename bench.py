@@ -331,7 +331,7 @@ def main():
         d = float(dt)
         # coverage checked every 10 iterations (a thin halo re-plans and replays, pcd_slab); slabs re-cut by class
         # cost after the second warm-up iteration (rebalance), so the timed region runs on the balanced plan
-        sd = SlabDenoiser(pos, nrm, max(args.k, args.k_update), transport=TorchTransport(), k_hint=args.k,
+        sd = SlabDenoiser(pos, nrm, max(args.k, args.k_update), transport=TorchTransport(),
                           seeding=args.seeding, check_every=10)
         del pos, nrm
         params = nat.make_params(k=args.k, k_update=args.k_update, d=d)

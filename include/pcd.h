@@ -74,6 +74,11 @@ int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, const fl
 /* The cell lattice pcd_grid_build would pick for xyz (origin = bbox minimum, cell edge), without building. */
 int pcd_grid_params(const float* xyz, int64_t n, int k_hint, float cell, float* origin3, float* cell_out,
                     void* stream);
+/* Another index over the SAME frozen snapshot as `src` (its points, in caller order) with another cell size (cell <= 0:
+ * ~k_hint/2 points per occupied cell).  The fused loop indexes its snapshot with cells of about its list cap
+ * (Processor picks k_hint = 2 x the cap): the re-anchoring searches then resolve fewer, fuller cells per query.
+ * Synchronises `stream`. */
+int pcd_grid_rebuild(const pcd_grid* src, int k_hint, float cell, void* stream, pcd_grid** out);
 int pcd_grid_destroy(pcd_grid* g);
 int pcd_grid_get_info(const pcd_grid* g, pcd_grid_info_t* out);
 /* perm[r] = original index of the r-th point in the grid's spatial (Morton) order; int32 device [n]. */

@@ -72,7 +72,12 @@ class Processor:
     # ------------------------------------------------------------------ fused loop
     def _fused_for(self, k_max: int) -> _nat.FusedDenoiser:
         if self._fused is None or self._fused.k_max < k_max:
-            self._fused = _nat.FusedDenoiser(self.selector.grid, k_max)
+            # the same frozen snapshot, indexed with cells of about one list cap of points (pcd_native.fused_k_hint)
+            grid = self.selector.grid
+            kh = _nat.fused_k_hint(k_max)
+            if kh and grid.k_hint != kh:
+                grid = grid.rebuild(kh)
+            self._fused = _nat.FusedDenoiser(grid, k_max)
         return self._fused
 
     def meanEdgeLength(self) -> torch.Tensor:

@@ -61,15 +61,37 @@ __global__ void k_sample(const float* __restrict__ xyz, int64_t n, int64_t strid
     out[3 * t + 2] = xyz[3 * i + 2];
 }
 
-__global__ void k_keys(const float* __restrict__ xyz, int64_t n, float ox, float oy, float oz, float inv_h,
+// Sort keys: the Morton code of the cell, refined by `sub` bits per axis of the point's position inside its cell
+// (kGridSub when every axis has at most 2^(21 - kGridSub) cells, else 0).  Morton order is hierarchical, so a cell's
+// points stay one contiguous run (cell key = key >> 3 sub), and inside it they follow the same space-filling curve:
+// rows that are neighbours in space are neighbours in memory at a finer grain than the search cell, which is what
+// the row-order gathers of the fused loop (anchor sets, NVT windows) feed on, and it lets the search cell be coarse.
+#ifndef PCD_GRID_SUB
+#define PCD_GRID_SUB 2
+#endif
+static constexpr int kGridSub = PCD_GRID_SUB;
+PCD_DEV int sub_coord(float p, float o, float inv_h, int c, int sub) {
+    const float f = fminf(fmaxf((p - o) * inv_h, -1.0e9f), 1.0e9f);   // as cell_coord
+    const float r = (f - (float)c) * (float)(1 << sub);                 // exact: f - floor(f), times a power of two
+    return min(max((int)floorf(r), 0), (1 << sub) - 1);
+}
+__global__ void k_keys(const float* __restrict__ xyz, int64_t n, float ox, float oy, float oz, float inv_h, int sub,
                        unsigned long long* __restrict__ keys, int32_t* __restrict__ vals) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const int cx = cell_coord(xyz[3 * i], ox, inv_h);
-    const int cy = cell_coord(xyz[3 * i + 1], oy, inv_h);
-    const int cz = cell_coord(xyz[3 * i + 2], oz, inv_h);
-    keys[i] = morton3(max(cx, 0), max(cy, 0), max(cz, 0));
+    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    const int cx = cell_coord(x, ox, inv_h), cy = cell_coord(y, oy, inv_h), cz = cell_coord(z, oz, inv_h);
+    const int fx = cx < 0 ? 0 : (cx << sub) | sub_coord(x, ox, inv_h, cx, sub);
+    const int fy = cy < 0 ? 0 : (cy << sub) | sub_coord(y, oy, inv_h, cy, sub);
+    const int fz = cz < 0 ? 0 : (cz << sub) | sub_coord(z, oz, inv_h, cz, sub);
+    keys[i] = morton3(fx, fy, fz);
     vals[i] = (int32_t)i;
+}
+
+// sorted fine keys -> cell keys
+__global__ void k_key_shift(unsigned long long* __restrict__ keys, int64_t n, int shift) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < n) keys[i] >>= shift;
 }
 
 __global__ void k_gather_sorted(const float* __restrict__ xyz, const int32_t* __restrict__ perm, int64_t n,
@@ -240,8 +262,8 @@ static int query_order(const GridView& g, const float* q, int64_t nq, hipStream_
     keys2 = reinterpret_cast<unsigned long long*>(base + off_k2);
     vals = reinterpret_cast<int32_t*>(base + off_v);
     order = reinterpret_cast<int32_t*>(base + off_o);
-    hipLaunchKernelGGL(k_keys, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, st, q, nq, g.ox, g.oy, g.oz, g.inv_h, keys,
-                       vals);
+    hipLaunchKernelGGL(k_keys, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, st, q, nq, g.ox, g.oy, g.oz, g.inv_h, 0,
+                       keys, vals);
     if (rocprim::radix_sort_pairs(base + off_t, tmp_bytes, keys, keys2, vals, order, (size_t)nq, 0u, end_bit, st) !=
         hipSuccess)
         return fail(PCD_ERR_HIP, "query order: rocprim::radix_sort_pairs failed");
@@ -398,12 +420,14 @@ int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, const fl
         free_tmp(); cleanup(); return fail(PCD_ERR_OOM, "pcd_grid_build: device allocation");
     }
     const dim3 blk(256), grd((unsigned)cdiv(n, 256));
-    hipLaunchKernelGGL(k_keys, grd, blk, 0, st, xyz, n, v.ox, v.oy, v.oz, v.inv_h, keys, vals);
+    const int sub = std::max({v.dx, v.dy, v.dz}) <= (1 << (21 - kGridSub)) ? kGridSub : 0;
+    hipLaunchKernelGGL(k_keys, grd, blk, 0, st, xyz, n, v.ox, v.oy, v.oz, v.inv_h, sub, keys, vals);
     (void)rocprim::radix_sort_pairs(nullptr, tmp_bytes, keys, keys2, vals, g->perm, (size_t)n, 0u, 63u, st);
     if (hipMalloc(&tmp, tmp_bytes) != hipSuccess) { free_tmp(); cleanup(); return fail(PCD_ERR_OOM, "sort temp"); }
     if (rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, keys2, vals, g->perm, (size_t)n, 0u, 63u, st) != hipSuccess) {
         free_tmp(); cleanup(); return fail(PCD_ERR_HIP, "rocprim::radix_sort_pairs failed");
     }
+    if (sub) hipLaunchKernelGGL(k_key_shift, grd, blk, 0, st, keys2, n, 3 * sub);
     hipLaunchKernelGGL(k_gather_sorted, grd, blk, 0, st, xyz, g->perm, n, g->pts);
     hipLaunchKernelGGL(k_sentinel, dim3(1), dim3(64), 0, st, g->pts + n);
     (void)hipMemsetAsync(cnt, 0, 16, st);
@@ -459,6 +483,29 @@ int pcd_grid_destroy(pcd_grid* g) {
     (void)hipFree(g->cellr);
     delete g;
     return PCD_OK;
+}
+
+// the snapshot back in caller order (pts[r] -> xyz[perm[r]])
+__global__ void k_unsort_xyz(const float4* __restrict__ pts, const int32_t* __restrict__ perm, int64_t n,
+                             float* __restrict__ xyz) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const float4 p = pts[r];
+    const int64_t i = perm[r];
+    xyz[3 * i] = p.x; xyz[3 * i + 1] = p.y; xyz[3 * i + 2] = p.z;
+}
+
+int pcd_grid_rebuild(const pcd_grid* src, int k_hint, float cell, void* stream, pcd_grid** out) {
+    PCD_CHECK_ARG(src && out, "null argument");
+    *out = nullptr;
+    hipStream_t st = as_stream(stream);
+    float* xyz = nullptr;
+    if (hipMalloc(&xyz, src->n * 3 * sizeof(float)) != hipSuccess) return fail(PCD_ERR_OOM, "pcd_grid_rebuild: xyz");
+    hipLaunchKernelGGL(k_unsort_xyz, dim3((unsigned)cdiv(src->n, 256)), dim3(256), 0, st, src->pts, src->perm, src->n, xyz);
+    const int rc = pcd_grid_build(xyz, src->n, k_hint, cell, nullptr, stream, out);   // (synchronises st)
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(xyz);
+    return rc;
 }
 
 int pcd_grid_get_info(const pcd_grid* g, pcd_grid_info_t* out) {

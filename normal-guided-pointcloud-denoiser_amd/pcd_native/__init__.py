@@ -47,6 +47,7 @@ _SIGS = {
     "pcd_denoise_params_size": (c_int, []),
     "pcd_grid_build": (c_int, [c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, POINTER(c_void_p)]),
     "pcd_grid_params": (c_int, [c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, c_void_p]),
+    "pcd_grid_rebuild": (c_int, [c_void_p, c_int, c_float, c_void_p, POINTER(c_void_p)]),
     "pcd_grid_destroy": (c_int, [c_void_p]),
     "pcd_grid_get_info": (c_int, [c_void_p, POINTER(_GridInfo)]),
     "pcd_grid_perm": (c_int, [c_void_p, c_void_p, c_void_p]),
@@ -191,7 +192,17 @@ class Grid:
                                ctypes.byref(h)), "pcd_grid_build")
         self.handle = h
         self.n = x.size(0)
+        self.k_hint = int(k_hint) if cell <= 0 else 0
         self._keep = None
+
+    def rebuild(self, k_hint: int) -> "Grid":
+        """A grid over this grid's own frozen snapshot with cells of ~k_hint/2 points (pcd_grid_rebuild)."""
+        h = c_void_p()
+        check(lib().pcd_grid_rebuild(self.handle, int(k_hint), 0.0, c_void_p(stream_ptr()), ctypes.byref(h)),
+              "pcd_grid_rebuild")
+        g = Grid.__new__(Grid)
+        g.handle, g.n, g.k_hint, g._keep = h, self.n, int(k_hint), None
+        return g
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -512,6 +523,19 @@ def mesh_vta(f: torch.Tensor, nv: int, out_dtype=torch.int64):
     check(lib().pcd_mesh_vta(ptr(f), 32 if f.dtype == torch.int32 else 64, nf, int(nv), ptr(vf), ptr(ni),
                              32 if out_dtype == torch.int32 else 64, c_void_p(stream_ptr())), "pcd_mesh_vta")
     return vf, ni
+
+
+def list_cap(k: int) -> int:
+    """Columns of the fused loop's stored lists for k = max(k, k_update) (denoise.hip list_cap)."""
+    return 8 if k <= 8 else 16 if k <= 16 else 32 if k <= 32 else 64
+
+
+def fused_k_hint(k_max: int) -> int:
+    """Cell size of the fused loop's snapshot index: about one list cap of points per occupied cell (k_hint = 2 x
+    the cap) for the anchored searches (cap <= 32).  Measured at 10M points, k = 32 (cap 32), iterations 6-25: 8 points
+    a cell 8.16 ms per iteration, 16 a cell 5.77 ms, 32 a cell 5.44 ms, 48 a cell 5.46 ms, 64 a cell 5.57 ms."""
+    cap = list_cap(k_max)
+    return 2 * cap if cap <= 32 else 0
 
 
 def grid_params(xyz: torch.Tensor, k_hint: int = 16, cell: float = 0.0):

@@ -239,7 +239,7 @@ class SlabDenoiser:
     recovery."""
 
     def __init__(self, snap_pos, snap_n, k_max, transport=None, halo=None, engine_factory=None, seeding=True,
-                 k_hint=32, check_every=1, halo_growth=2.0, max_replans=4, weights=None):
+                 k_hint=None, check_every=1, halo_growth=2.0, max_replans=4, weights=None):
         self.t = transport or LocalTransport()
         rank, world = self.t.rank, self.t.world
         if world > 1:
@@ -253,7 +253,8 @@ class SlabDenoiser:
                 h.fill_(default_halo(snap_pos, k_max))
             halo = float(self.t.broadcast_(h)) if world > 1 else float(h)
         self.snap_pos, self.snap_n = snap_pos, snap_n
-        self.k_max, self.k_hint, self.seeding = k_max, k_hint, seeding
+        # cell lattice of the ranks' snapshot indices: the fused loop's (pcd_native.fused_k_hint) unless given
+        self.k_max, self.k_hint, self.seeding = k_max, k_hint or nat.fused_k_hint(k_max) or 32, seeding
         self.engine_factory = engine_factory
         self.check_every, self.halo_growth, self.max_replans = int(check_every), float(halo_growth), int(max_replans)
         self.replans = 0

@@ -301,7 +301,7 @@ def test_anchors_survive_reload(golden, gpu):
     pos = torch.empty((N, 3), device=gpu); n = torch.empty((N, 3), device=gpu)
     a.store(pos, n)
     outs = []
-    for fused in (a, nat.FusedDenoiser(proc.selector.grid, 32)):
+    for fused in (a, nat.FusedDenoiser(a.grid, 32)):   # (same grid: exact distance ties break by its rank order)
         fused.load(pos, n)                   # anchored (a) vs fresh (dense re-anchoring) from the same state
         fused.iterate(params, 2)
         p2 = torch.empty((N, 3), device=gpu); n2 = torch.empty((N, 3), device=gpu)

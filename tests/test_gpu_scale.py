@@ -51,7 +51,7 @@ def run_pair(pos, nrm, k, iterations, dev, check_every=True):
     d = 2 * float(proc.meanEdgeLength())
     params = nat.make_params(k=k, k_update=8, d=d)
     a = proc._fused_for(k)
-    b = nat.FusedDenoiser(proc.selector.grid, k)
+    b = nat.FusedDenoiser(a.grid, k)   # the same snapshot index: exact distance ties break by its rank order
     a.load(proc.graph.pos, proc.graph.n)
     b.load(proc.graph.pos, proc.graph.n)
     b.set_seeding(False)
