@@ -76,8 +76,14 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 #define PCD_NVT1_HALO 256
 #endif
 static constexpr int kWinHalo = PCD_NVT1_HALO;          // NVT1
-static constexpr int kWinHaloNvt2 = 512;
-static constexpr int kWinHaloPhase = 128;
+#ifndef PCD_NVT2_HALO
+#define PCD_NVT2_HALO 512
+#endif
+#ifndef PCD_PHASE_HALO
+#define PCD_PHASE_HALO 128
+#endif
+static constexpr int kWinHaloNvt2 = PCD_NVT2_HALO;
+static constexpr int kWinHaloPhase = PCD_PHASE_HALO;
 template <int H, int BS = 256> struct WinSize { static constexpr int rows = BS + 2 * H; };
 #ifndef PCD_NVT_BS
 #define PCD_NVT_BS 256
@@ -275,7 +281,8 @@ template <int K, int KA>
 __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const float4* __restrict__ pos, int64_t N,
                                                           RowMap rm, int kstore, const float4* __restrict__ anc,
                                                           const int32_t* __restrict__ alist,
-                                                          int32_t* __restrict__ idx, uint8_t* __restrict__ fail) {
+                                                          int32_t* __restrict__ idx, uint8_t* __restrict__ fail,
+                                                          int32_t* __restrict__ redo, unsigned* __restrict__ redo_cnt) {
     static_assert(KA == 2 * K && KA <= 64, "anchor lists hold twice the list cap; 6 slot bits");
     __shared__ uint32_t s_r[KA * kAnchorBS];
     const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * kAnchorBS + threadIdx.x;
@@ -330,8 +337,20 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
             }
         }
     }
-    if (t0 < rm.nq) fail[t0] = failed ? 1 : 0;   // -> ordered redo list (rocprim::select): redo rows stay in
-                                                 // spatial order, so the waves in flight on an XCD share its L2
+    if (t0 < rm.nq) fail[t0] = failed ? 1 : 0;
+    if (redo) {
+        // the failed rows straight onto the redo list: one atomic per wave, the wave's rows in row order (blocks run
+        // roughly in order, so the list stays spatially coherent for the re-anchoring waves)
+        const bool f = t0 < rm.nq && failed;
+        const unsigned long long m = __ballot(f);
+        if (m) {
+            const int lane = (int)(threadIdx.x & 63);
+            unsigned base = 0;
+            if (lane == 0) base = atomicAdd(redo_cnt, (unsigned)__popcll(m));
+            base = (unsigned)__shfl((int)base, 0);
+            if (f) redo[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)rm(t0);
+        }
+    }
 }
 
 // NVT1 + eigh + VU smoothing over the stored lists (lane per row); checks every list entry and, for spatial slabs,
@@ -817,6 +836,9 @@ static int select_rows(pcd_denoiser* dn, const RowMap& rm, int32_t* list, unsign
 #ifndef PCD_RQ_GRID
 #define PCD_RQ_GRID 4096
 #endif
+#ifndef PCD_REDO_ATOMIC
+#define PCD_REDO_ATOMIC 0    // 1: the anchor test appends its failed rows to the redo list itself (no select pass)
+#endif
 #ifndef PCD_NVT1_OVERLAP
 #define PCD_NVT1_OVERLAP 0   // measured: the side-stream NVT1 slows the re-anchoring more than it hides
 #endif
@@ -867,8 +889,9 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
                                dn->anc, dn->alist, dn->idx, nullptr, nullptr, dn->spill, spill_cnt);                   \
         } else {                                                                                                       \
             hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd_anc, dim3(kAnchorBS), 0, st, gv, P, N, rm, kstore,        \
-                               dn->anc, dn->alist, dn->idx, dn->fail);                                                 \
-            if ((rc = select_rows(dn, rm, dn->redo, redo_cnt, st)) != PCD_OK) return rc;                               \
+                               dn->anc, dn->alist, dn->idx, dn->fail, PCD_REDO_ATOMIC && !overlap ? dn->redo : nullptr, \
+                               redo_cnt);                                                                              \
+            if ((!PCD_REDO_ATOMIC || overlap) && (rc = select_rows(dn, rm, dn->redo, redo_cnt, st)) != PCD_OK) return rc; \
             if (overlap) {                                                                                             \
                 PCD_HIP(hipEventRecord(dn->fork, st));                                                                 \
                 PCD_HIP(hipStreamWaitEvent(dn->side, dn->fork, 0));                                                    \
