@@ -529,7 +529,9 @@ __global__ __launch_bounds__(kNvtBS) void k_nvt2(const float4* __restrict__ pos,
     }
 }
 
-struct RedC { double sx, sy, sz, cnt; };
+// One flat-reduction block's partial: f64 sums and count of its rows, the box of those rows (for the pruned max
+// distance pass), and whether that pass must scan the block (set by k_centre).
+struct RedC { double sx, sy, sz, cnt; float lo[3], hi[3]; int scan, pad; };
 
 // The k_u neighbour rows of point i, all loads in flight together (KU = compile-time bound on ku).
 template <int KU>
@@ -550,14 +552,14 @@ PCD_DEV void gather_rows(const float4* __restrict__ pos, const int32_t* __restri
 static constexpr int kRowsInFlight = PCD_ROWS_IN_FLIGHT;
 template <int KU>
 PCD_DEV void gather_rows_batch(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N, RowMap rm,
-                               const uint8_t* __restrict__ cls, int c, int ku, int64_t t, int64_t G,
+                               const uint8_t* __restrict__ cls, int c, int ku, int64_t t, int64_t G, int64_t end,
                                bool (&on)[kRowsInFlight], float4 (&v)[kRowsInFlight][KU]) {
     int64_t ii[kRowsInFlight];
 #pragma unroll
     for (int r = 0; r < kRowsInFlight; ++r) {
         const int64_t tt = t + r * G;
-        ii[r] = tt < rm.nq ? rm(tt) : 0;
-        on[r] = tt < rm.nq;
+        ii[r] = tt < end ? rm(tt) : 0;
+        on[r] = tt < end;
     }
 #pragma unroll
     for (int r = 0; r < kRowsInFlight; ++r) on[r] = on[r] && cls[ii[r]] == c;
@@ -565,33 +567,57 @@ PCD_DEV void gather_rows_batch(const float4* __restrict__ pos, const int32_t* __
     for (int r = 0; r < kRowsInFlight; ++r) gather_rows<KU>(pos, idx, N, on[r] ? ii[r] : 0, ku, v[r]);
 }
 
+// Block b of the flat reductions owns the CONTIGUOUS active rows [b R, (b + 1) R), R = ceil(nq / blocks): rows are
+// in spatial order, so the box of a block's rows is small and the max-distance pass can skip the blocks whose box
+// provably holds no farther row than another block's nearest bound (k_centre).
+PCD_DEV void part_range(int64_t nq, int64_t& beg, int64_t& end) {
+    const int64_t R = (nq + gridDim.x - 1) / gridDim.x;
+    beg = (int64_t)blockIdx.x * R;
+    end = beg + R < nq ? beg + R : nq;
+}
+
 template <int KU>
 __global__ __launch_bounds__(256) void k_class_rows_sum(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N, RowMap rm,
                                  int ku, const uint8_t* __restrict__ cls, int c, RedC* __restrict__ part) {
     double sx = 0, sy = 0, sz = 0, cnt = 0;
-    const int64_t G = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < rm.nq; t += kRowsInFlight * G) {
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    int64_t beg, end;
+    part_range(rm.nq, beg, end);
+    for (int64_t t = beg + threadIdx.x; t < end; t += kRowsInFlight * 256) {
         bool on[kRowsInFlight];
         float4 v[kRowsInFlight][KU];
-        gather_rows_batch<KU>(pos, idx, N, rm, cls, c, ku, t, G, on, v);
+        gather_rows_batch<KU>(pos, idx, N, rm, cls, c, ku, t, 256, end, on, v);
 #pragma unroll
         for (int r = 0; r < kRowsInFlight; ++r) {
             if (!on[r]) continue;
 #pragma unroll
             for (int u = 0; u < KU; ++u)
-                if (u < ku) { sx += v[r][u].x; sy += v[r][u].y; sz += v[r][u].z; }
+                if (u < ku) {
+                    sx += v[r][u].x; sy += v[r][u].y; sz += v[r][u].z;
+                    lo[0] = fminf(lo[0], v[r][u].x); lo[1] = fminf(lo[1], v[r][u].y); lo[2] = fminf(lo[2], v[r][u].z);
+                    hi[0] = fmaxf(hi[0], v[r][u].x); hi[1] = fmaxf(hi[1], v[r][u].y); hi[2] = fmaxf(hi[2], v[r][u].z);
+                }
             cnt += ku;
         }
     }
     __shared__ double s[4][256];
+    __shared__ float sb[6][256];
     s[0][threadIdx.x] = sx; s[1][threadIdx.x] = sy; s[2][threadIdx.x] = sz; s[3][threadIdx.x] = cnt;
+    for (int a = 0; a < 3; ++a) { sb[a][threadIdx.x] = lo[a]; sb[3 + a][threadIdx.x] = hi[a]; }
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w)
+        if ((int)threadIdx.x < w) {
             for (int a = 0; a < 4; ++a) s[a][threadIdx.x] += s[a][threadIdx.x + w];
+            for (int a = 0; a < 3; ++a) {
+                sb[a][threadIdx.x] = fminf(sb[a][threadIdx.x], sb[a][threadIdx.x + w]);
+                sb[3 + a][threadIdx.x] = fmaxf(sb[3 + a][threadIdx.x], sb[3 + a][threadIdx.x + w]);
+            }
+        }
         __syncthreads();
     }
-    if (threadIdx.x == 0) part[blockIdx.x] = RedC{s[0][0], s[1][0], s[2][0], s[3][0]};
+    if (threadIdx.x == 0)
+        part[blockIdx.x] = RedC{s[0][0], s[1][0], s[2][0], s[3][0], {sb[0][0], sb[1][0], sb[2][0]},
+                                {sb[3][0], sb[4][0], sb[5][0]}, 1, 0};
 }
 
 // pass 2: the partials -> (Σx, Σy, Σz, count) in f64 (what a multi-rank caller all-reduces).
@@ -609,29 +635,69 @@ __global__ void k_part_reduce(const RedC* __restrict__ part, int np, double* __r
     if (threadIdx.x == 0) for (int q = 0; q < 4; ++q) red[q] = s[q][0];
 }
 
-// pass 3: centre = Σ / count (the reference's f32 mean over all E rows, Denoiser.py:106), delta reset.
-__global__ void k_centre(const double* __restrict__ red, float* __restrict__ g) {
+// pass 3: centre = Σ / count (the reference's f32 mean over all E rows, Denoiser.py:106), delta reset, and the blocks
+// pass 4 must scan: with d_b = max over axes of the farther of |hi_a - c_a|, |c_a - lo_a| (a row attains each face
+// of the box, so some row of block b lies at least d_b from the centre) and U_b = the distance to the farthest box
+// corner (no row of b lies farther), every block with U_b below max_b d_b is skipped: it cannot hold the maximum.
+// Bounds in f64 with a relative margin far above the fp32 rounding of pass 4's squared distances.
+__global__ void k_centre(const double* __restrict__ red, float* __restrict__ g, RedC* __restrict__ part, int np) {
+    __shared__ float s_c[3];
+    __shared__ double s_lb[256];
     if (threadIdx.x == 0) {
         const double c = red[3];
         g[0] = (float)(red[0] / c);
         g[1] = (float)(red[1] / c);
         g[2] = (float)(red[2] / c);
         reinterpret_cast<unsigned int*>(g)[3] = 0u;
+        s_c[0] = g[0]; s_c[1] = g[1]; s_c[2] = g[2];
+    }
+    __syncthreads();
+    if (!part) return;
+    auto bounds = [&](const RedC& p, double& lb2, double& ub2) {
+        lb2 = 0.0; ub2 = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            const double f = fmax((double)p.hi[a] - (double)s_c[a], (double)s_c[a] - (double)p.lo[a]);
+            lb2 = fmax(lb2, f * f);
+            ub2 += f * f;
+        }
+    };
+    double lb = 0.0;
+    for (int b = threadIdx.x; b < np; b += blockDim.x) {
+        if (!(part[b].cnt > 0)) continue;
+        double l, u;
+        bounds(part[b], l, u);
+        lb = fmax(lb, l);
+    }
+    s_lb[threadIdx.x] = lb;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) s_lb[threadIdx.x] = fmax(s_lb[threadIdx.x], s_lb[threadIdx.x + w]);
+        __syncthreads();
+    }
+    const double LB = s_lb[0] * (1.0 - 1e-4);
+    for (int b = threadIdx.x; b < np; b += blockDim.x) {
+        double l, u;
+        bounds(part[b], l, u);
+        part[b].scan = part[b].cnt > 0 && !(u * (1.0 + 1e-4) < LB) ? 1 : 0;
     }
 }
 
 // pass 4: delta = max ||v_j - centre|| over the same rows (Denoiser.py:107), atomicMax on the f32 bits.  The max is
-// taken over d² and rooted once (sqrt is monotone); rows kRowsInFlight at a time as in pass 1.
+// taken over d² and rooted once (sqrt is monotone); rows kRowsInFlight at a time as in pass 1, only in the blocks
+// k_centre left to scan.
 template <int KU>
 __global__ __launch_bounds__(256) void k_class_rows_maxdist(const float4* __restrict__ pos, const int32_t* __restrict__ idx, int64_t N,
-                                     RowMap rm, int ku, const uint8_t* __restrict__ cls, int c, float* __restrict__ g) {
+                                     RowMap rm, int ku, const uint8_t* __restrict__ cls, int c, float* __restrict__ g,
+                                     const RedC* __restrict__ part) {
+    if (part && !part[blockIdx.x].scan) return;       // (block-uniform)
     const Vec3 ctr = v3(g[0], g[1], g[2]);
     float mx2 = 0.f;
-    const int64_t G = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < rm.nq; t += kRowsInFlight * G) {
+    int64_t beg, end;
+    part_range(rm.nq, beg, end);
+    for (int64_t t = beg + threadIdx.x; t < end; t += kRowsInFlight * 256) {
         bool on[kRowsInFlight];
         float4 v[kRowsInFlight][KU];
-        gather_rows_batch<KU>(pos, idx, N, rm, cls, c, ku, t, G, on, v);
+        gather_rows_batch<KU>(pos, idx, N, rm, cls, c, ku, t, 256, end, on, v);
 #pragma unroll
         for (int r = 0; r < kRowsInFlight; ++r) {
             if (!on[r]) continue;
@@ -741,6 +807,8 @@ struct pcd_denoiser {
     int32_t* idx = nullptr;
     uint8_t* cls = nullptr;
     RedC* part = nullptr;
+    int part_ph = -1;             // phase whose rows the flat-reduction partials (boxes) describe, -1: none
+    int scan_ph = -1;             // phase whose max-distance block flags k_centre set, -1: none
     double* red = nullptr;        // 4 doubles per phase: (Σx, Σy, Σz, count) of the global reductions
     float* gscal = nullptr;       // 4 floats per phase: centre xyz, delta bits
     int* err = nullptr;           // device error word (see k_knn_nvt1), checked by store() / check()
@@ -776,6 +844,9 @@ struct pcd_denoiser {
 
 #ifndef PCD_NUM_PART
 #define PCD_NUM_PART 1024
+#endif
+#ifndef PCD_MAXDIST_PRUNE
+#define PCD_MAXDIST_PRUNE 1   // the max-distance pass skips the blocks whose row box cannot hold the maximum
 #endif
 static const int kNumPart = PCD_NUM_PART;   // blocks of the flat reductions (grid-stride), = their partials
 // Timing events per iteration: start, after the anchor test (+ redo-list select), after the re-anchoring search,
@@ -990,11 +1061,17 @@ static int stage_sum(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, doub
 #undef PCD_RS
     hipLaunchKernelGGL(k_part_reduce, dim3(1), dim3(256), 0, st, dn->part, kNumPart, red4);
     PCD_LAUNCH_CHECK();
+    dn->part_ph = ph;
+    dn->scan_ph = -1;
     return PCD_OK;
 }
 
 static int stage_centre(pcd_denoiser* dn, int ph, const double* red4, hipStream_t st) {
-    hipLaunchKernelGGL(k_centre, dim3(1), dim3(64), 0, st, red4, dn->gscal + 4 * ph);
+    // (the pruning needs this phase's partials: stage_sum of the same phase on the same positions)
+    const bool prune = PCD_MAXDIST_PRUNE && dn->part_ph == ph;
+    hipLaunchKernelGGL(k_centre, dim3(1), dim3(256), 0, st, red4, dn->gscal + 4 * ph, prune ? dn->part : nullptr,
+                       kNumPart);
+    dn->scan_ph = prune ? ph : -1;
     PCD_LAUNCH_CHECK();
     return PCD_OK;
 }
@@ -1003,7 +1080,8 @@ static int stage_centre(pcd_denoiser* dn, int ph, const double* red4, hipStream_
 static int stage_maxdist(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, float* red1, hipStream_t st) {
     float* gs = dn->gscal + 4 * ph;
 #define PCD_MD(C) hipLaunchKernelGGL(k_class_rows_maxdist<C>, dim3(kNumPart), dim3(256), 0, st, dn->pos[dn->cur], \
-                                     dn->idx, dn->n, dn->rowmap(), p->k_update, dn->cls, p->phase_class[ph], gs)
+                                     dn->idx, dn->n, dn->rowmap(), p->k_update, dn->cls, p->phase_class[ph], gs,   \
+                                     dn->scan_ph == ph ? dn->part : nullptr)
     switch (knn_cap(p->k_update)) {
         case 8: PCD_MD(8); break;
         case 16: PCD_MD(16); break;
@@ -1018,6 +1096,7 @@ static int stage_maxdist(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, 
 
 static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, const float* red1, hipStream_t st) {
     const RowMap rm = dn->rowmap();
+    dn->part_ph = dn->scan_ph = -1;     // positions change: the partials' boxes no longer describe them
     float* gs = dn->gscal + 4 * ph;
     if (red1) hipLaunchKernelGGL(k_copy_delta, dim3(1), dim3(64), 0, st, red1, gs + 3);
     const int kind = p->phase_kind[ph], c = p->phase_class[ph];
@@ -1124,6 +1203,7 @@ int pcd_denoiser_load(pcd_denoiser* dn, const float* pos, const float* n, void* 
                        dn->g->perm, dn->n, dn->pos[0], dn->nrm, dn->orig);
     PCD_LAUNCH_CHECK();
     dn->cur = 0;
+    dn->part_ph = dn->scan_ph = -1;
     dn->loaded = true;
     dn->iterated = false;
     dn->unit_nrm = false;         // the caller's normals: the general vote margin until the first finish
@@ -1137,6 +1217,7 @@ int pcd_denoiser_set_rows(pcd_denoiser* dn, const int32_t* rows, int64_t n_rows)
     PCD_CHECK_ARG(n_rows >= 0 && n_rows <= dn->n, "n_rows out of range");
     dn->rows = rows;
     dn->n_rows = rows ? n_rows : 0;
+    dn->part_ph = dn->scan_ph = -1;
     return PCD_OK;
 }
 
@@ -1172,6 +1253,7 @@ int pcd_denoiser_unpack(pcd_denoiser* dn, int field, const int32_t* rows, int64_
     PCD_CHECK_ARG(f != nullptr, "bad field");
     PCD_CHECK_ARG(n == 0 || (rows && in4), "null rows / buffer");
     if (n == 0) return PCD_OK;
+    dn->part_ph = dn->scan_ph = -1;
     hipLaunchKernelGGL(k_unpack, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, as_stream(stream), f, rows, n,
                        reinterpret_cast<const float4*>(in4));
     PCD_LAUNCH_CHECK();

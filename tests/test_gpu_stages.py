@@ -246,3 +246,40 @@ def test_eigh3_batch_lapack_matches_host_build(gpu):
 def test_eigh3_batch_rejects_bad_solver(gpu):
     with pytest.raises(ValueError):
         nat.eigh3_batch(torch.zeros((4, 6), device=gpu), 2)
+
+
+# ------------------------------------------------------------------ the flat phase's global centre and delta
+@pytest.mark.parametrize("n", [200_000, 2_000_000])
+def test_flat_centre_and_pruned_delta(gpu, n):
+    """Denoiser.py:106-107 through the fused stages: centre = f32 mean of the k_u neighbour rows of every flat point,
+    delta = the largest distance from it over the same rows.  The max-distance pass skips the reduction blocks whose
+    row box cannot hold the maximum (k_centre): delta must equal the exhaustive fp32 maximum bit for bit."""
+    from test_gpu_scale import bunny_cloud
+    pos, nrm = bunny_cloud(n, 5, 0.005)
+    pos_t, n_t = pos.to(gpu), nrm.to(gpu)
+    grid = nat.Grid(pos_t, k_hint=64)
+    fd = nat.FusedDenoiser(grid, K)
+    fd.load(pos_t, n_t)
+    p = nat.make_params(k=K, k_update=KU, d=0.01)
+    fd.stage(p, nat.STAGE_KNN_NVT1)
+    fd.stage(p, nat.STAGE_NVT2)
+    red4 = torch.zeros(4, dtype=torch.float64, device=gpu)
+    red1 = torch.zeros(1, dtype=torch.float32, device=gpu)
+    fd.stage(p, nat.STAGE_PHASE_SUM, 0, red4)
+    fd.stage(p, nat.STAGE_PHASE_CENTRE, 0, red4)
+    fd.stage(p, nat.STAGE_PHASE_MAXDIST, 0, red1)
+    fd.stage(p, nat.STAGE_FINISH)                        # (no phase applied: the positions are the ones reduced)
+    q = torch.empty_like(pos_t)
+    cls = torch.empty(n, dtype=torch.int64, device=gpu)
+    fd.store(q, None, cls)
+    lists = fd.lists(K)[:, :KU]
+    flat = cls == 0
+    assert flat.float().mean() > 0.3
+    rows = q[lists[flat].reshape(-1)]                     # every E row of Denoiser.py:106 (k_u per flat point)
+    c64 = rows.double().sum(0) / rows.shape[0]
+    np.testing.assert_allclose(red4[:3].cpu().numpy() / red4[3].item(), c64.cpu().numpy(), rtol=1e-9)
+    assert red4[3].item() == rows.shape[0]
+    ctr = (red4[:3] / red4[3]).float()
+    d = rows - ctr
+    d2 = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]    # the kernel's fp32 order (sq3)
+    assert red1.item() == torch.sqrt(d2.max()).item()
