@@ -276,7 +276,10 @@ PCD_DEV bool anchor_holds(float d2k, Vec3 q, float4 a) {
 #ifndef PCD_ANCHOR_SORT
 #define PCD_ANCHOR_SORT oddeven_sort
 #endif
-static constexpr int kAnchorBS = 128;
+#ifndef PCD_ANCHOR_BS
+#define PCD_ANCHOR_BS 128
+#endif
+static constexpr int kAnchorBS = PCD_ANCHOR_BS;
 template <int K, int KA>
 __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const float4* __restrict__ pos, int64_t N,
                                                           RowMap rm, int kstore, const float4* __restrict__ anc,
@@ -902,7 +905,7 @@ static int select_rows(pcd_denoiser* dn, const RowMap& rm, int32_t* list, unsign
 // search (pcd_qknn.h) of the rows that failed it -- or of every row when there are no anchors (of this KA) yet --
 // and the exact-key wave search (pcd_wknn.h) for the few rows it spills.
 #ifndef PCD_RQ_RDENSE
-#define PCD_RQ_RDENSE 1.2f   // (1.45: first iteration 35.3 ms; 1.3: 31.7; 1.2: 29.7; 1.1: 27.5 but the next iterations fail more)
+#define PCD_RQ_RDENSE 1.1f   // first iteration at 10M: 1.45 35.3 ms, 1.3 31.7, 1.2 29.7 (16-point cells); 1.2 26.0-26.7, 1.1 24.3 (32-point cells)
 #endif
 #ifndef PCD_RQ_GRID
 #define PCD_RQ_GRID 4096
