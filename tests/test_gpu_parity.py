@@ -116,6 +116,50 @@ def test_knn_duplicates_and_ties(gpu):
         assert list(idx[r]) == list(order), r
 
 
+@pytest.mark.parametrize("k_hint", [8, 64, 256])
+def test_grid_rebuild_indexes_the_same_snapshot(fan, gpu, k_hint):
+    """pcd_grid_rebuild: another cell size over the SAME frozen snapshot (the fused loop's grid, Processor._fused_for)
+    -- every public query answers identically (exact lists and d², ties by original index), and its rank order is a
+    permutation of the snapshot."""
+    snap = fan["pos0"]
+    g0 = nat.Grid(T(snap, gpu), k_hint=16)
+    g1 = g0.rebuild(k_hint)
+    assert g1.n == g0.n and g1.k_hint == k_hint
+    perm = g1.perm().cpu().numpy()
+    assert (np.sort(perm) == np.arange(len(snap))).all()
+    rng = np.random.default_rng(k_hint)
+    q = T((snap + rng.normal(0, 0.01, snap.shape)).astype(np.float32), gpu)
+    for k in (1, 16, 32):
+        i0, d0 = g0.knn(q, k, with_d2=True)
+        i1, d1 = g1.knn(q, k, with_d2=True)
+        assert torch.equal(i0, i1) and torch.equal(d0, d1), k
+    info0, info1 = g0.info(), g1.info()
+    assert info0["origin"] == info1["origin"]
+    assert (info1["cell"] > info0["cell"]) == (k_hint > 16)
+
+
+def test_fused_loop_grid_is_one_list_cap_a_cell(fan, gpu):
+    """Processor._fused_for indexes the frozen snapshot with k_hint = 2 x the list cap (pcd_native.fused_k_hint), a
+    separate grid from the Selector's, and the loop on it matches the loop on the Selector's grid: the same kNN sets;
+    exact distance ties (fandisk's regular sampling has them) break by each grid's rank order, which can reorder two
+    equidistant neighbours in the NVT sums -- rounding-level differences only."""
+    pc = Pointcloud(T(fan["pos0"], gpu).clone(), T(fan["n0"], gpu).clone())
+    proc = Processor(pc, k_hint=16)
+    fused = proc._fused_for(32)
+    assert fused.grid.k_hint == 64 and fused.grid is not proc.selector.grid
+    params = nat.make_params(k=32, k_update=8, d=float(fan["d"]))
+    outs = []
+    for f in (fused, nat.FusedDenoiser(proc.selector.grid, 32)):
+        f.load(proc.graph.pos, proc.graph.n)
+        f.iterate(params, 3)
+        p = torch.empty_like(proc.graph.pos)
+        f.store(p)
+        outs.append(p.cpu().numpy())
+    bbox = float(np.linalg.norm(fan["pos0"].max(0) - fan["pos0"].min(0)))
+    dev = np.linalg.norm(outs[0] - outs[1], axis=1) / bbox
+    assert np.median(dev) == 0.0 and np.percentile(dev, 99) <= 1e-6, (np.percentile(dev, 99), dev.max())
+
+
 def test_knn_rejects_k_larger_than_n(gpu):
     grid = nat.Grid(torch.rand(5, 3, device=gpu))
     with pytest.raises(ValueError):
