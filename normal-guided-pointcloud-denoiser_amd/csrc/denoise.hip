@@ -722,13 +722,29 @@ __global__ void k_copy_delta(const float* __restrict__ from, float* __restrict__
 #ifndef PCD_PHASE_WIN
 #define PCD_PHASE_WIN 1
 #endif
+// SPLIT (the fused loop's three Gauss-Seidel phases over every row, one class each): no phase copies the rows it
+// does not move.  Every phase reads pin and writes its own class's rows to pout, so after phase ph a row's current
+// position is in pout if its class was moved by an earlier phase (bit cls of `moved`) and in pin otherwise; after the
+// last phase every row is in pout.  Same arithmetic on the same inputs as the copying phases (the parity tests
+// compare the two paths bitwise: test_gpu_slab's world-1 slab runs the copying stages).
+struct SplitRows {
+    const float4* a;             // positions before this iteration's phases
+    const float4* b;             // rows moved by the earlier phases of this iteration
+    const uint8_t* cls;
+    uint32_t moved;
+    PCD_DEV Vec3 operator()(int64_t j) const {
+        const float4 q = ((moved >> cls[j]) & 1u) ? b[j] : a[j];
+        return v3(q.x, q.y, q.z);
+    }
+};
+
 template <int KIND, int KU>
 __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, float4* __restrict__ pout,
                                                 const float4* __restrict__ fn, const float4* __restrict__ edge,
                                                 const int32_t* __restrict__ idx, int64_t N, RowMap rm, int ku,
                                                 const uint8_t* __restrict__ cls, int c, const float* __restrict__ g,
                                                 float d, float alpha, int win, int copy_others,
-                                                const float4* __restrict__ orig, float clampg) {
+                                                const float4* __restrict__ orig, float clampg, uint32_t moved) {
     // the flat phase moves most rows: its neighbour rows come from an LDS window of pin / fn around the block
     constexpr bool WIN = PCD_PHASE_WIN && (KIND == PCD_STEP_FLAT);
     __shared__ float4 s_pos[WIN ? WinSize<kWinHaloPhase, 256>::rows : 1], s_fn[WIN ? WinSize<kWinHaloPhase, 256>::rows : 1];
@@ -738,13 +754,14 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
     const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
-    const float4 p4 = pin[i];
-    if (cls[i] != c) {                  // Gauss-Seidel: every phase copies the others; Jacobi: only the first
-        if (copy_others) pout[i] = p4;
+    if (cls[i] != c) {                  // Gauss-Seidel: every phase copies the others; Jacobi / SPLIT: only the first
+        if (copy_others) pout[i] = pin[i];
         return;
     }
+    const float4 p4 = pin[i];
     const Vec3 vi = v3(p4.x, p4.y, p4.z);
     const Rows4 P{pin}, F{fn};
+    const SplitRows PS{pin, pout, cls, moved};
     // the update list: block 0 (pcd_lists.h), 16-B loads (8-B in the windowed flat phase: load_list_clamped8)
     RegNbC<KU> nb;
     if constexpr (WIN) load_list_clamped8<KU>(idx, N, i, ku, nb.l);
@@ -754,6 +771,9 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
         o = step_flat<KU>(WinRows<kWinHaloPhase, 256>{pin, s_pos, lo}, WinRows<kWinHaloPhase, 256>{fn, s_fn, lo}, vi, F(i), ku,
                           nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
     else if (KIND == PCD_STEP_FLAT) o = step_flat<KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
+    else if (moved && KIND == PCD_STEP_EDGE) o = step_edge<KU, 4>(PS, F, vi, Rows4{edge}(i), ku, nb, d, alpha);
+    else if (moved && KIND == PCD_STEP_FEATURE) o = step_feature<false, KU, 4>(PS, F, vi, F(i), ku, nb, 1.f, d, alpha);
+    else if (moved && KIND == PCD_STEP_CORNER) o = step_corner<KU, 4>(PS, F, vi, ku, nb, d, alpha);
     else if (KIND == PCD_STEP_EDGE) o = step_edge<KU, 4>(P, F, vi, Rows4{edge}(i), ku, nb, d, alpha);
     else if (KIND == PCD_STEP_FEATURE) o = step_feature<false, KU, 4>(P, F, vi, F(i), ku, nb, 1.f, d, alpha);
     else if (KIND == PCD_STEP_NEW) o = step_feature<true, KU>(P, F, vi, F(i), ku, nb, __uint_as_float(((const unsigned*)g)[3]), d, alpha);
@@ -847,6 +867,9 @@ struct pcd_denoiser {
 
 #ifndef PCD_NUM_PART
 #define PCD_NUM_PART 1024
+#endif
+#ifndef PCD_PHASE_SPLIT
+#define PCD_PHASE_SPLIT 1     // copy-free Gauss-Seidel phases in pcd_denoiser_iterate (k_phase SplitRows)
 #endif
 #ifndef PCD_MAXDIST_PRUNE
 #define PCD_MAXDIST_PRUNE 1   // the max-distance pass skips the blocks whose row box cannot hold the maximum
@@ -1097,7 +1120,10 @@ static int stage_maxdist(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, 
     return PCD_OK;
 }
 
-static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, const float* red1, hipStream_t st) {
+// split: the fused loop's copy-free phases (k_phase SPLIT; pcd_denoiser_iterate decides), moved = the classes the
+// earlier phases of this iteration moved into pos[cur ^ 1]; cur flips after the last phase only.
+static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, const float* red1, hipStream_t st,
+                       bool split = false, uint32_t moved = 0) {
     const RowMap rm = dn->rowmap();
     dn->part_ph = dn->scan_ph = -1;     // positions change: the partials' boxes no longer describe them
     float* gs = dn->gscal + 4 * ph;
@@ -1106,10 +1132,10 @@ static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, co
     const float a = p->phase_alpha[ph];
     float4* pin = dn->pos[dn->cur];
     float4* pout = dn->pos[dn->cur ^ 1];
-    const int copy_others = (!p->jacobi || ph == 0) ? 1 : 0;
+    const int copy_others = split ? 0 : (!p->jacobi || ph == 0) ? 1 : 0;
     if (rm.nq > 0) {
         const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
-#define PCD_PH2(KD, C) hipLaunchKernelGGL((k_phase<KD, C>), grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, dn->n, rm, p->k_update, dn->cls, c, gs, p->d, a, dn->windows, copy_others, dn->orig, p->clamp_global)
+#define PCD_PH2(KD, C) hipLaunchKernelGGL((k_phase<KD, C>), grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, dn->n, rm, p->k_update, dn->cls, c, gs, p->d, a, dn->windows, copy_others, dn->orig, p->clamp_global, moved)
 #define PCD_PH(KD)                                                                                                     \
     switch (knn_cap(p->k_update)) {                                                                                    \
         case 8: PCD_PH2(KD, 8); break;                                                                                 \
@@ -1129,7 +1155,7 @@ static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, co
 #undef PCD_PH2
         PCD_LAUNCH_CHECK();
     }
-    if (!p->jacobi) dn->cur ^= 1;    // Jacobi: every phase reads the same input; the swap happens at finish
+    if (split ? ph == p->nphases - 1 : !p->jacobi) dn->cur ^= 1;   // Jacobi: the swap happens at finish
     return PCD_OK;
 }
 
@@ -1437,6 +1463,12 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
         if (ev) PCD_HIP(hipEventRecord(ev[4], st));
         if ((rc = stage_k2(dn, p, st)) != PCD_OK) return rc;
         if (ev) PCD_HIP(hipEventRecord(ev[5], st));
+        // copy-free phases when three Gauss-Seidel phases move the three classes of every row once each and only the
+        // first phase reduces globally (its reductions read the positions before any phase)
+        const bool split = PCD_PHASE_SPLIT && !p->jacobi && !dn->rows && p->nphases == 3 &&
+                           ((1u << p->phase_class[0]) | (1u << p->phase_class[1]) | (1u << p->phase_class[2])) == 7u &&
+                           !phase_is_global(p, 1) && !phase_is_global(p, 2);
+        uint32_t moved = 0;
         for (int ph = 0; ph < p->nphases; ++ph) {
             if (phase_is_global(p, ph)) {
                 double* red4 = dn->red + 4 * ph;
@@ -1444,7 +1476,8 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
                 if ((rc = stage_centre(dn, ph, red4, st)) != PCD_OK) return rc;
                 if ((rc = stage_maxdist(dn, p, ph, nullptr, st)) != PCD_OK) return rc;
             }
-            if ((rc = stage_apply(dn, p, ph, nullptr, st)) != PCD_OK) return rc;
+            if ((rc = stage_apply(dn, p, ph, nullptr, st, split, split ? moved : 0u)) != PCD_OK) return rc;
+            moved |= 1u << p->phase_class[ph];
             if (ev) PCD_HIP(hipEventRecord(ev[6 + ph], st));
         }
         if (ev)
