@@ -237,9 +237,14 @@ static constexpr int kRqMaxCells = 4096;
 static constexpr int kRqChunk = PCD_RQ_CELLS;  // cells per chunk (per group)
 template <int W> struct RqCPL { static constexpr int n = kRqChunk / W; };   // cells per lane per chunk
 static constexpr int kRqChunkLog2 = kRqChunk == 64 ? 6 : kRqChunk == 128 ? 7 : 8;
+#ifndef PCD_RQ_MAP
+#define PCD_RQ_MAP 1024        // flattened rows of a chunk mapped to their cell in LDS (0: binary search per row)
+#endif
+static constexpr int kRqMap = PCD_RQ_MAP;
 struct RqCells {            // per-group LDS scratch for one chunk of cells
     uint32_t start[kRqChunk];
     uint32_t end_incl[kRqChunk];
+    uint8_t cellof[kRqMap > 0 ? kRqMap : 4];   // cell (slot in the chunk) of each flattened candidate row
 };
 // Where a scan reads its cells and candidate rows from: GridSrc is the grid in global memory (brick hash probes,
 // brick cell blocks, snapshot rows; a row's rank is its index).  A source only has to resolve a lane's cells to row
@@ -340,6 +345,16 @@ PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo
             wc->start[hl * CPL + u] = cr[u].x;
             wc->end_incl[hl * CPL + u] = excl + loc[u];
         }
+        // the cell of every flattened row, so a row finds its cell with one LDS read instead of a binary search over
+        // the chunk (~40 VALU per row): each lane fills the runs of its own cells
+        const bool mapped = kRqMap > 0 && total <= (uint32_t)kRqMap;   // (group-uniform)
+        if (mapped) {
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                const uint32_t b = excl + (u ? loc[u - 1] : 0u), e = excl + loc[u];
+                for (uint32_t k = b; k < e; ++k) wc->cellof[k] = (uint8_t)(hl * CPL + u);
+            }
+        }
         wave_sync();
 #if defined(PCD_EXP_RQ) && PCD_EXP_RQ == 2    // timing experiment: cell phase only (results wrong)
         if (total != 0x7FFFFFFF) { wave_sync(); continue; }
@@ -351,11 +366,16 @@ PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo
 #pragma unroll
             for (int u = 0; u < kRqRows; ++u) {
                 const uint32_t j = j0 + (uint32_t)(u * W + hl);
-                int a = 0, b = kRqChunk - 1;
+                int a = 0;
+                if (mapped) {
+                    a = j < total ? (int)wc->cellof[j] : 0;
+                } else {
+                    int b = kRqChunk - 1;
 #pragma unroll
-                for (int it = 0; it < kRqChunkLog2; ++it) {
-                    const int m = (a + b) >> 1;
-                    if (wc->end_incl[m] > j) b = m; else a = m + 1;
+                    for (int it = 0; it < kRqChunkLog2; ++it) {
+                        const int m = (a + b) >> 1;
+                        if (wc->end_incl[m] > j) b = m; else a = m + 1;
+                    }
                 }
                 r[u] = j < total ? wc->start[a] + (j - (a ? wc->end_incl[a - 1] : 0u)) : 0u;
             }
