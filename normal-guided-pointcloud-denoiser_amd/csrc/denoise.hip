@@ -284,8 +284,7 @@ template <int K, int KA>
 __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const float4* __restrict__ pos, int64_t N,
                                                           RowMap rm, int kstore, const float4* __restrict__ anc,
                                                           const int32_t* __restrict__ alist,
-                                                          int32_t* __restrict__ idx, uint8_t* __restrict__ fail,
-                                                          int32_t* __restrict__ redo, unsigned* __restrict__ redo_cnt) {
+                                                          int32_t* __restrict__ idx, uint8_t* __restrict__ fail) {
     static_assert(KA == 2 * K && KA <= 64, "anchor lists hold twice the list cap; 6 slot bits");
     __shared__ uint32_t s_r[KA * kAnchorBS];
     const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * kAnchorBS + threadIdx.x;
@@ -340,19 +339,46 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
             }
         }
     }
-    if (t0 < rm.nq) fail[t0] = failed ? 1 : 0;
-    if (redo) {
-        // the failed rows straight onto the redo list: one atomic per wave, the wave's rows in row order (blocks run
-        // roughly in order, so the list stays spatially coherent for the re-anchoring waves)
-        const bool f = t0 < rm.nq && failed;
-        const unsigned long long m = __ballot(f);
-        if (m) {
-            const int lane = (int)(threadIdx.x & 63);
-            unsigned base = 0;
-            if (lane == 0) base = atomicAdd(redo_cnt, (unsigned)__popcll(m));
-            base = (unsigned)__shfl((int)base, 0);
-            if (f) redo[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)rm(t0);
-        }
+    if (t0 < rm.nq) fail[t0] = failed ? 1 : 0;   // -> the redo list (k_compact_fail)
+}
+
+// The anchor test's failed rows -> the redo list: each block takes 4,096 consecutive flags (16 per thread, one 16-B
+// load), writes its failed rows in row order at a base it takes with ONE atomic -- blocks start roughly in order, so
+// the list stays spatially coherent for the re-anchoring waves (what rocprim::select's strict order bought, at a
+// tenth of its time: 10 MB of flags).
+static constexpr int kCompactBS = 256, kCompactPer = 16;
+__global__ __launch_bounds__(kCompactBS) void k_compact_fail(const uint8_t* __restrict__ fail, RowMap rm,
+                                                             int32_t* __restrict__ list, unsigned* __restrict__ cnt) {
+    __shared__ uint32_t s_w[kCompactBS / 64];
+    __shared__ uint32_t s_base;
+    const int64_t f0 = ((int64_t)blockIdx.x * kCompactBS + threadIdx.x) * kCompactPer;
+    uint32_t bits = 0;
+    if (f0 + kCompactPer <= rm.nq) {
+        const uint4 v = *reinterpret_cast<const uint4*>(fail + f0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bits |= ((w[q] >> (8 * b)) & 0xFFu) ? 1u << (4 * q + b) : 0u;
+    } else {
+        for (int k = 0; k < kCompactPer; ++k)
+            if (f0 + k < rm.nq && fail[f0 + k]) bits |= 1u << k;
+    }
+    const uint32_t n = (uint32_t)__popc(bits);
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    const uint32_t incl = lane_scan_incl<64>(n);
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kCompactBS / 64; ++w) { before += w < wv ? s_w[w] : 0u; total += s_w[w]; }
+    if (threadIdx.x == 0) s_base = total ? atomicAdd(cnt, total) : 0u;
+    __syncthreads();
+    uint32_t o = s_base + before + incl - n;
+    while (bits) {
+        const int k = __ffs(bits) - 1;
+        bits &= bits - 1;
+        list[o++] = (int32_t)rm(f0 + k);
     }
 }
 
@@ -933,8 +959,8 @@ static int select_rows(pcd_denoiser* dn, const RowMap& rm, int32_t* list, unsign
 #ifndef PCD_RQ_GRID
 #define PCD_RQ_GRID 4096
 #endif
-#ifndef PCD_REDO_ATOMIC
-#define PCD_REDO_ATOMIC 0    // 1: the anchor test appends its failed rows to the redo list itself (no select pass)
+#ifndef PCD_REDO_COMPACT
+#define PCD_REDO_COMPACT 1   // the redo list by k_compact_fail (one atomic per 4,096 rows); 0: rocprim::select (row order)
 #endif
 #ifndef PCD_NVT1_OVERLAP
 #define PCD_NVT1_OVERLAP 0   // measured: the side-stream NVT1 slows the re-anchoring more than it hides
@@ -965,7 +991,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
     const dim3 grd_rq((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), dense ? 16384 : PCD_RQ_GRID));
     const dim3 grd_wave((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), PCD_REDO_GRID));
-    const dim3 grd_anc((unsigned)cdiv(rm.nq, kAnchorBS));
+    const dim3 grd_anc((unsigned)cdiv(rm.nq, kAnchorBS)), grd_cmp((unsigned)cdiv(rm.nq, kCompactBS * kCompactPer));
     int rc = PCD_OK;
     // Dense (no anchors): every row is re-anchored, then NVT1 runs over all rows.  Seeded: the anchor test, then
     // NVT1 of the certified rows on the side stream while this stream re-anchors the others (latency-bound wave
@@ -986,9 +1012,10 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
                                dn->anc, dn->alist, dn->idx, nullptr, nullptr, dn->spill, spill_cnt);                   \
         } else {                                                                                                       \
             hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd_anc, dim3(kAnchorBS), 0, st, gv, P, N, rm, kstore,        \
-                               dn->anc, dn->alist, dn->idx, dn->fail, PCD_REDO_ATOMIC && !overlap ? dn->redo : nullptr, \
-                               redo_cnt);                                                                              \
-            if ((!PCD_REDO_ATOMIC || overlap) && (rc = select_rows(dn, rm, dn->redo, redo_cnt, st)) != PCD_OK) return rc; \
+                               dn->anc, dn->alist, dn->idx, dn->fail);                                                 \
+            if (PCD_REDO_COMPACT && !overlap)                                                                          \
+                hipLaunchKernelGGL(k_compact_fail, grd_cmp, dim3(kCompactBS), 0, st, dn->fail, rm, dn->redo, redo_cnt); \
+            else if ((rc = select_rows(dn, rm, dn->redo, redo_cnt, st)) != PCD_OK) return rc;                          \
             if (overlap) {                                                                                             \
                 PCD_HIP(hipEventRecord(dn->fork, st));                                                                 \
                 PCD_HIP(hipStreamWaitEvent(dn->side, dn->fork, 0));                                                    \
