@@ -77,7 +77,7 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 #endif
 static constexpr int kWinHalo = PCD_NVT1_HALO;          // NVT1
 #ifndef PCD_NVT2_HALO
-#define PCD_NVT2_HALO 512
+#define PCD_NVT2_HALO 256   // (A/B at 10M after the round-3 changes: 256 0.870 ms, 384 0.882, 512 0.889)
 #endif
 #ifndef PCD_PHASE_HALO
 #define PCD_PHASE_HALO 128
