@@ -475,7 +475,9 @@ def main():
         "config": {"workload": ("configs[4]: synthetic %dM-point bunny-sampled surface, spatial slabs with RCCL halo"
                                 % (total_points // 1_000_000) if mode == "slab" else
                                 "configs[3] headline substitute: 10M-pt bunny-sampled cloud (xyzrgb_dragon.obj is "
-                                "a missing blob)") + ", k=32, k_u=8, 1 iteration per step",
+                                "a missing blob)" if args.points == 10_000_000 else
+                                "NOT the headline: %.4gM-pt bunny-sampled cloud per GPU" % (args.points / 1e6))
+                               + ", k=%d, k_u=%d, 1 iteration per step" % (args.k, args.k_update),
                    "points_per_gpu": total_points // world, "k": args.k, "k_update": args.k_update,
                    "global_points": total_points,
                    "parallelism": {"single": "single", "replicas": f"replicas x{world}",
