@@ -892,7 +892,7 @@ struct pcd_denoiser {
 };
 
 #ifndef PCD_NUM_PART
-#define PCD_NUM_PART 1024
+#define PCD_NUM_PART 2048
 #endif
 #ifndef PCD_PHASE_SPLIT
 #define PCD_PHASE_SPLIT 1     // copy-free Gauss-Seidel phases in pcd_denoiser_iterate (k_phase SplitRows)
