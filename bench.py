@@ -45,6 +45,10 @@ from Pointcloud.Modules.Object import Pointcloud, sample_surface  # noqa: E402
 from Pointcloud.Modules.Processor import Processor  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# what the PMC byte counts are (profiles/r3/calib_traffic.json): memory-side requests of the L2, so Infinity-Cache
+# (MALL) hits count too -- an upper bound on HBM bytes, not HBM bytes
+TRAFFIC_KIND = ("L2-miss bytes per launch: rocprofv3 FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE; Infinity-Cache "
+                "hits included, so an upper bound on HBM traffic")
 
 
 # Per-stage bound, as the rocprofv3 counters of profiles/ show it: VALU = VALU-issue-bound (>= 1/2 of
@@ -246,6 +250,32 @@ def cpsd_bench(dev, cpu, points=50_000, iterations=50):
     return out
 
 
+def slab_world1_bench(pos, nrm, params, args, fused_ms):
+    """The multi-GPU driver (pcd_slab.SlabDenoiser: one pcd_slab_iterate call per iteration, the coverage check and
+    checkpoint every 10 iterations, as the N-GPU bench runs it) at one rank on the headline workload, timed like the
+    main line (warm-up, then the steps between synchronisations): its overhead over the fused loop at N = 1."""
+    from pcd_slab import LocalTransport, SlabDenoiser
+    sd = SlabDenoiser(pos, nrm, max(args.k, args.k_update), transport=LocalTransport(), seeding=args.seeding,
+                      check_every=10)
+    for _ in range(args.warmup):
+        sd.iterate(params, 1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sd.iterate(params, 1)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / args.steps * 1e3
+    sd.check()
+    stages = sd.iterate_timed(params)
+    out = {"ms_per_step": round(ms, 4), "ratio_to_fused_loop": round(ms / fused_ms, 4),
+           "stage_ms": {k: round(v, 4) for k, v in stages.items()},
+           "note": "SlabDenoiser + LocalTransport, one pcd_slab_iterate call per iteration, coverage check and "
+                   "checkpoint every 10 iterations inside the timed steps"}
+    del sd
+    torch.cuda.empty_cache()
+    return out
+
+
 def measured_traffic(points, k, ms_per_step):
     """HBM bytes per iteration from profiles/traffic.json (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch, the
     gfx950 correction of MI355X_MICROARCH.md), summed over the iteration's kernels, against 8 TB/s."""
@@ -260,7 +290,7 @@ def measured_traffic(points, k, ms_per_step):
         return None
     b = float(tj["per_iteration_bytes"])
     return {"bytes_per_iteration": b, "achieved": round(b / (ms_per_step / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(b / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "unit": "GB/s", "frac": round(b / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "kind": TRAFFIC_KIND,
             "source": tj.get("source", "profiles/traffic.json")}
 
 
@@ -291,6 +321,8 @@ def main():
                     help="skip the mesh-update and CPSD-driver measurements (mesh_update, cpsd)")
     ap.add_argument("--no-rebalance", dest="rebalance", action="store_false",
                     help="slab mode: keep the equal-count cut (default: re-cut by class cost after warm-up 2)")
+    ap.add_argument("--no-slab1", dest="slab1", action="store_false",
+                    help="skip the slab_world1 block (the multi-GPU driver at one rank on the same workload)")
     ap.add_argument("--no-ten", dest="ten", action="store_false",
                     help="skip the ten_iteration_ms measurement (fresh cloud, 10 iterations incl. the first)")
     args = ap.parse_args()
@@ -498,8 +530,19 @@ def main():
         "roofline": {"kernel": "K1 stage (kNN + NVT1): " + " + ".join(k1_names), "bound": "valu+latency",
                      "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": traffic, "alg_bytes_per_launch": k1_bytes, "avg_launch_ms": round(knn_ms, 4)},
+                     "traffic": traffic, "traffic_kind": TRAFFIC_KIND,
+                     "measured_frac": (round(traffic / (knn_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                                       if traffic and knn_ms == knn_ms else None),
+                     "alg_bytes_per_launch": k1_bytes, "avg_launch_ms": round(knn_ms, 4)},
+        "bound_statement": ("every per-iteration kernel is VALU- or memory-latency-bound (SQ counters, DESIGN.md §3): "
+                            "the iteration moves ~0.28 of the 8 TB/s HBM peak by the PMC counters; `frac` is the "
+                            "SURVEY §8(d) algorithmic-bytes model (each neighbour attribute read counted per use, "
+                            "most of them served by LDS windows and L2), `measured_frac` the counted bytes"),
     }
+    if out["measured_traffic"]:
+        out["iteration_roofline"]["measured_frac"] = out["measured_traffic"]["frac"]
+    if rank == 0 and world == 1 and args.slab1:
+        out["slab_world1"] = slab_world1_bench(pos, nrm, params, args, ms_per_step)
     if rank == 0 and world == 1 and args.extras:
         out["mesh_update"] = mesh_bench(dev, not args.no_cpu_baseline)
         out["cpsd"] = cpsd_bench(dev, not args.no_cpu_baseline)

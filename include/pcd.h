@@ -193,7 +193,7 @@ typedef struct {
 /* sizeof(pcd_denoise_params) as this library was built: a binding checks its mirror against it (a struct that
  * is shorter than the library's would be read past its end). */
 int pcd_denoise_params_size(void);
-/* g: the frozen snapshot, at most 2^28 points (268M; larger clouds run as spatial slabs, pcd_slab). */
+/* g: the frozen snapshot, fewer than 2^27 points (134M; larger clouds run as spatial slabs, pcd_slab). */
 int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out);
 int pcd_denoiser_destroy(pcd_denoiser* dn);
 /* pos, n: caller rows [N][3] (original order, N = grid n) -> internal spatial order */
@@ -257,7 +257,7 @@ int pcd_denoiser_probe_store(pcd_denoiser* dn, float* nvt2_eig4, void* stream);
  *   per iteration: KNN_NVT1 -> exchange FN -> NVT2 -> per phase [flat/new: PHASE_SUM(red=double[4]) ->
  *   all-reduce sum -> PHASE_CENTRE(red) -> PHASE_MAXDIST(red=float[1]) -> all-reduce max] -> PHASE_APPLY(red or
  *   null) -> exchange POS -> FINISH.  pcd_denoiser_iterate runs the same sequence with no exchange. */
-enum { PCD_FIELD_POS = 0, PCD_FIELD_NRM = 1, PCD_FIELD_FN = 2 };
+enum { PCD_FIELD_POS = 0, PCD_FIELD_NRM = 1, PCD_FIELD_FN = 2, PCD_FIELD_EDGE = 3 };
 enum { PCD_STAGE_KNN_NVT1 = 0, PCD_STAGE_NVT2 = 1, PCD_STAGE_PHASE_SUM = 2, PCD_STAGE_PHASE_CENTRE = 3,
        PCD_STAGE_PHASE_MAXDIST = 4, PCD_STAGE_PHASE_APPLY = 5, PCD_STAGE_FINISH = 6 };
 /* rows: device int32 [n_rows] of spatial-order rows (ascending), kept by the caller; null = all rows. */
@@ -268,11 +268,72 @@ int pcd_denoiser_set_coverage(pcd_denoiser* dn, const float* lo3, const float* h
  * float[1] delta, nullable = local value). */
 int pcd_denoiser_stage(pcd_denoiser* dn, const pcd_denoise_params* p, int stage, int phase, void* red,
                        void* stream);
-/* state rows <-> packed device float4 buffers (field PCD_FIELD_*; POS = current positions).  FN rows unpacked
+/* state rows <-> packed device float4 buffers (field PCD_FIELD_*; POS = current positions, EDGE = NVT2's edge vectors,
+ * written by a test to feed the edge phase the reference's own).  FN rows unpacked
  * between K1 and NVT2 must be another rank's K1 output (unit vectors: NVT2's vote margin assumes it). */
 int pcd_denoiser_pack(pcd_denoiser* dn, int field, const int32_t* rows, int64_t n, float* out4, void* stream);
 int pcd_denoiser_unpack(pcd_denoiser* dn, int field, const int32_t* rows, int64_t n, const float* in4,
                         void* stream);
+
+/* ---- the CPSD ("Martin") comparison driver in one call (PostProcessing.ipynb:1041-1062) ----
+ * Per iteration on the loaded state: kNN(k_update) lists of the current positions, the radius-r selection over the
+ * frozen snapshot (scipy query_ball_point membership, Selector.py:214-233) with the normal-filtered NVT + VU smoothing
+ * (Processor.getMartinFeatureDecomposition, Processor.py:102-108) and PVT, VU features (Decompositionor.py:84-85), then
+ * flat_step / edge_step / corner_step with alpha[3] and the per-step clamp, Jacobi across classes, the global clamp
+ * ||pos - pos at load|| < d, n := f_n.  No host synchronisation per iteration; one at the end of the call. */
+typedef struct {
+    float r;             /* radius of the selection, the notebook's r = d                               */
+    float rho;           /* vote angle of both normal filters, 0.9                                      */
+    float tau;           /* VU smoothing and VU-feature threshold, 0.3                                  */
+    float damp;          /* VU smoothing dampening, 3                                                   */
+    float d;             /* global clamp (PostProcessing.ipynb:1060)                                    */
+    float step_clamp;    /* per-step displacement clamp, d * 20000                                      */
+    float alpha[3];      /* flat, edge, corner step: 0.1, 1, 1                                          */
+    int k_update;        /* update kNN size, 8                                                          */
+} pcd_cpsd_params;
+int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* p, int iterations, void* stream);
+
+/* ---- spatial slabs in one call per iteration (the RCCL communicator, halo exchange and scalar
+ * all-reduces live in the library; PyTorch only sets up the ranks) ----
+ * A pcd_comm is the slab transport: RCCL over xGMI (pcd_comm_create from a unique id rank 0 made with pcd_comm_id and
+ * the caller broadcast), or host callbacks (pcd_comm_create_host: any transport the caller has, e.g. gloo in tests;
+ * every exchange is staged through pinned host memory and handed to the callback). */
+typedef struct pcd_comm pcd_comm;
+enum { PCD_DT_F32 = 0, PCD_DT_F64 = 1, PCD_DT_I32 = 2 };
+enum { PCD_OP_SUM = 0, PCD_OP_MAX = 1 };
+typedef struct {
+    void* user;
+    /* Exchange float4 rows with npeers peers: to peers[q] send rows [send_off[q], send_off[q+1]) of `send`, from it
+     * receive rows [recv_off[q], recv_off[q+1]) into `recv` (HOST memory, 4 floats a row).  Return 0 on success. */
+    int (*exchange)(void* user, int npeers, const int* peers, const float* send, const int64_t* send_off, float* recv,
+                    const int64_t* recv_off);
+    /* In-place all-reduce of count elements of dtype PCD_DT_* with PCD_OP_* over every rank (HOST memory). */
+    int (*allreduce)(void* user, void* buf, int count, int dtype, int op);
+} pcd_host_transport;
+/* bytes of an RCCL unique id (ncclUniqueId) */
+int pcd_comm_id_bytes(void);
+/* rank 0: a fresh RCCL unique id into id_out [pcd_comm_id_bytes()] for the caller to broadcast */
+int pcd_comm_id(void* id_out);
+/* every rank (collective, on its own HIP device): the RCCL communicator of `world` ranks from rank 0's id */
+int pcd_comm_create(const void* id, int world, int rank, pcd_comm** out);
+int pcd_comm_create_host(const pcd_host_transport* t, int world, int rank, pcd_comm** out);
+int pcd_comm_destroy(pcd_comm* c);
+/* in-place all-reduce of device scalars (the flat phase's Σ and δ, Denoiser.py:106-107), stream-ordered */
+int pcd_allreduce_scalars(pcd_comm* c, void* buf, int count, int dtype, int op, void* stream);
+/* Halo routes of this rank's denoiser: for each of npeers peers (host arrays), n_send[q] own rows to send and
+ * n_recv[q] halo rows to receive; send_rows / recv_rows: device int32 spatial-order rows, peer after peer (copied).
+ * own_lo3 / own_hi3 (host, nullable): the OWNED slab (no halo) -- with it, NVT2 and the phases run the rows whose
+ * k-ball stays strictly inside it while an exchange is in flight.  Synchronises `stream`. */
+int pcd_denoiser_set_routes(pcd_denoiser* dn, int npeers, const int* peers, const int64_t* n_send,
+                            const int32_t* send_rows, const int64_t* n_recv, const int32_t* recv_rows,
+                            const float* own_lo3, const float* own_hi3, void* stream);
+/* one field (PCD_FIELD_*) of the send rows -> the peers' halo rows, stream-ordered */
+int pcd_halo_exchange(pcd_denoiser* dn, pcd_comm* c, int field, void* stream);
+/* `iterations` slab iterations of Processor.denoise's body (Processor.py:123-139) over the active rows: K1, f_n
+ * exchange, NVT2, the phases with their all-reduces and position exchanges, n := f_n -- one call, every exchange
+ * overlapped with the rows that need no halo data (the exchange runs on a stream of the library's own; later
+ * calls on this denoiser wait for it).  Same result bit for bit as the staged sequence above. */
+int pcd_slab_iterate(pcd_denoiser* dn, pcd_comm* c, const pcd_denoise_params* p, int iterations, void* stream);
 
 /* ------------------------------------------------------------------ normal orientation (host) */
 /* GraphBuilder.flipNormals: Kruskal MST on cost 1-|n_i·n_j| over the directed edge list (a[e] -> b[e],
@@ -297,8 +358,12 @@ int pcd_host_vu_smooth(const float* w, const float* v, const float* n, int64_t m
  * pos / n [.][3] -> t6 [m][6] (a00, a01, a02, a11, a12, a22); the fused kernels' vote and sums, on the host. */
 int pcd_host_nvt_tensor(const float* pos, const float* n, const int64_t* ci, const int64_t* off, const int64_t* nbr,
                         int64_t m, float rho, float* t6);
-/* a9 [m][3][3] row-major, b3 [m][3] -> x3 [m][3], ok [m] (0 when a pivot is exactly zero, x untouched = 0) */
+/* a9 [m][3][3] row-major, b3 [m][3] -> x3 [m][3] = inv_ex(A) b as the position steps compute it, ok [m] (0 when
+ * inv_ex reports info != 0, i.e. an exactly zero pivot; x untouched = 0) */
 int pcd_host_solve3(const float* a9, const float* b3, int64_t m, float* x3, int32_t* ok);
+/* torch.linalg.inv_ex (Denoiser.py:43, 80, 163, 210) restated for 3x3: a9 [m][3][3] -> inv9 [m][3][3], ok [m] as
+ * above (inv untouched = 0 where ok = 0).  The position steps' arithmetic (pcd_device.h inv3_ref), on the host. */
+int pcd_host_inv3(const float* a9, int64_t m, float* inv9, int32_t* ok);
 
 #ifdef __cplusplus
 }

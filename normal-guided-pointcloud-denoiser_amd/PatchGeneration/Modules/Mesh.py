@@ -28,13 +28,32 @@ def vertex_triangle_adjacency(f: np.ndarray, nv: int):
 
 class Mesh:
     def __init__(self, v, f, noise_factor=0, f2f=None, vta=None, gt=None):
+        self._topo = {}           # device copies of the faces and the adjacency, per precision
         self.v = v
         self.f = f
         self.noise_factor = noise_factor
         self.f2f = f2f
         self.vta = vta            # igl (VF, NI); None: built on the device on first use (pcd_mesh_vta)
         self.gt = gt
-        self._topo = {}           # device copies of the faces and the adjacency, per precision (they never change)
+
+    # assigning the faces or the adjacency drops the device copies built from them
+    @property
+    def f(self):
+        return self._f
+
+    @f.setter
+    def f(self, value):
+        self._f = value
+        self._topo = {}
+
+    @property
+    def vta(self):
+        return self._vta
+
+    @vta.setter
+    def vta(self, value):
+        self._vta = value
+        self._topo = {}
 
     @classmethod
     def readFile(cls, file_path: str) -> "Mesh":
@@ -54,22 +73,28 @@ class Mesh:
     def getVertexTriangleAdjacency(self):
         if self.vta is None:
             vf, ni = self._topology(False)[1:]
-            self.vta = (vf.cpu().numpy(), ni.cpu().numpy())
+            self._vta = (vf.cpu().numpy(), ni.cpu().numpy())   # (the device copies it came from stay valid)
         return self.vta
 
     def _topology(self, fp32: bool):
         """(faces, VF, NI) on the device, int32 for the fp32 path, int64 for fp64; the adjacency is the caller's vta
-        when one was given, else built on the device."""
-        key = (bool(fp32), id(self.f), np.shape(self.f))
-        if key not in self._topo:
+        when one was given, else built on the device.  Cached per precision together with a host copy of the faces
+        it was built from: an in-place edit of self.f (same object, new contents) rebuilds it."""
+        key = bool(fp32)
+        hit = self._topo.get(key)
+        if hit is not None and not np.array_equal(hit[0], self.f):
+            hit = None
+        if hit is None:
             it = torch.int32 if fp32 else torch.int64
-            fd = torch.as_tensor(np.ascontiguousarray(self.f)).to(_nat.device()).to(it).contiguous()
+            f_host = np.array(self.f, copy=True)
+            fd = torch.as_tensor(np.ascontiguousarray(f_host)).to(_nat.device()).to(it).contiguous()
             if self.vta is not None:
                 vf, ni = (torch.as_tensor(np.ascontiguousarray(a)).to(fd.device).to(it) for a in self.vta)
             else:
                 vf, ni = _nat.mesh_vta(fd, len(self.v), out_dtype=it)
-            self._topo[key] = (fd, vf.contiguous(), ni.contiguous())
-        return self._topo[key]
+            hit = (f_host, fd, vf.contiguous(), ni.contiguous())
+            self._topo[key] = hit
+        return hit[1:]
 
     def updateVertices(self, n, k=15, fp32: bool = False):
         """Mesh.py:377-418: k Jacobi sweeps, in place on self.v.  fp32=True runs the fp32 kernel (float4 rows, int32

@@ -34,7 +34,9 @@ class Noise:
                         dtype=torch.float32).to(gt.device) * std
         offset = r if noise_direction == 1 else self.graph.n * r[:, 0, None]
         if noise_type == 1:
-            gdev = gt.device if generator is None else generator.device
+            # the reference draws torch_randperm(n) on the CPU default generator (Noise.py:56); a caller generator
+            # draws on its own device
+            gdev = "cpu" if generator is None else generator.device
             drop = torch.randperm(n, generator=generator, device=gdev)[:int(n * (1 - noise_level))].to(gt.device)
             offset[drop] = 0
         self.setNoise(gt + offset, keepNormals)

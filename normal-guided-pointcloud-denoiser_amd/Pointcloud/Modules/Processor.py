@@ -137,19 +137,34 @@ class Processor:
         g.n = n_out.to(device=g.pos.device, dtype=g.pos.dtype)
 
     def cpsdDenoise(self, iterations: int = 50, d: float = None, alphas=(0.1, 1.0, 1.0), rho: float = 0.9,
-                    tau: float = 0.3, step_clamp_factor: float = 20000.0, k_update: int = 8):
-        """The CPSD ("Martin") comparison driver of the thesis results (PostProcessing.ipynb:1041-1062), on the device
-        op by op: per iteration getMartinFeatureDecomposition(r=d) (radius selection of the CURRENT positions against
-        the frozen snapshot, normal-filtered NVT, VU smoothing, normal-filtered PVT), VU classes (tau), kNN(k_update),
-        then flat_step / edge_step (PVT smallest eigenvector) / corner_step with alphas and the per-step clamp at
-        d * step_clamp_factor, all from the iteration's input positions (temp_pos = pos.clone()), and the GLOBAL clamp
-        against the positions at the start of the call (mask = ||temp_pos - original_pos|| < d).  graph.pos is updated
-        in place (masked), graph.n rebound to f_n.  d defaults to 2 x the mean kNN(6) edge length."""
+                    tau: float = 0.3, step_clamp_factor: float = 20000.0, k_update: int = 8, fused: bool = True):
+        """The CPSD ("Martin") comparison driver of the thesis results (PostProcessing.ipynb:1041-1062): per iteration
+        getMartinFeatureDecomposition(r=d) (radius selection of the CURRENT positions against the frozen snapshot,
+        normal-filtered NVT, VU smoothing, normal-filtered PVT), VU classes (tau), kNN(k_update), then flat_step /
+        edge_step (PVT smallest eigenvector) / corner_step with alphas and the per-step clamp at d * step_clamp_factor,
+        all from the iteration's input positions (temp_pos = pos.clone()), and the GLOBAL clamp against the positions at
+        the start of the call (mask = ||temp_pos - original_pos|| < d).  graph.pos is updated in place (masked),
+        graph.n rebound to f_n.  d defaults to 2 x the mean kNN(6) edge length.
+        fused (default): the whole loop in one library call (pcd_cpsd_iterate, every step on the device); False: the
+        same operators op by op through the drop-in classes (the cross-check)."""
         g = self.graph
         GeneralUtils.validateAttributes(g, ["pos", "n"])
         if d is None:
             d = 2 * float(self.meanEdgeLength())
         d = float(d)
+        if fused:
+            dn = self._fused_for(k_update)
+            dn.load(g.pos, g.n)
+            dn.cpsd_iterate(_nat.make_cpsd_params(r=d, d=d, rho=rho, tau=tau, step_clamp=d * step_clamp_factor,
+                                                  alphas=alphas, k_update=k_update), iterations)
+            dev = _nat.device()
+            pos_out = torch.empty((g.num_nodes, 3), dtype=torch.float32, device=dev)
+            n_out = torch.empty((g.num_nodes, 3), dtype=torch.float32, device=dev)
+            dn.store(pos_out, n_out)
+            with torch.no_grad():
+                g.pos.copy_(pos_out.to(g.pos.dtype))          # in place: keeps pointcloud.v aliased
+            g.n = n_out.to(device=g.pos.device, dtype=g.pos.dtype)
+            return
         original_pos = g.pos.clone()
         den = self.denoiser
         for _ in range(iterations):

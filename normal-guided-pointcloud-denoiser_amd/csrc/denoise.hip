@@ -31,7 +31,7 @@ namespace pcd {
 int knn_cap(int k);
 
 // Element i of a column whose base is uniform: a 32-bit byte offset (i * sizeof(T) < 4 GiB, checked on the host:
-// N < 2^28 for the anchored path) lets the load take the base in SGPRs and one offset VGPR (global_load ... saddr),
+// N < 2^27, pcd_denoiser_create: the blocked lists take 32 B x N) lets the load take the base in SGPRs and one offset VGPR (global_load ... saddr),
 // where 64-bit per-lane addresses cost a multiply-add and moves per column.
 template <class T>
 PCD_DEV const T* at32(const T* base, int64_t i) {
@@ -165,12 +165,29 @@ struct Cover {
     }
 };
 
+// Spatial slabs: the rank's OWN slab (the points it owns, no halo).  K1 marks every active row whose k-ball is not
+// strictly inside it: only those rows can list a halo row (every snapshot point strictly inside the owned slab on
+// the cut axis is owned -- slabs are contiguous ranges of the sorted axis key), so the NVT2 / phase passes of the
+// other rows need no halo data and run while the halo exchange is in flight (pcd_slab_iterate).  flag null: off.
+struct Band {
+    Cover box;
+    uint8_t* flag;    // [active rows]: 1 = may read a halo row
+    PCD_DEV void mark(int64_t t, Vec3 q, float d2) const { if (flag) flag[t] = box.holds(q, d2) ? 0 : 1; }
+};
+// Row selection of a pass: flag null -> every active row; else the active rows t with flag[t] == want.
+struct RowSel {
+    const uint8_t* flag;
+    int want;
+    PCD_DEV bool take(int64_t t) const { return !flag || (int)flag[t] == want; }
+};
+
 // K1 epilogue (every kNN variant): store the list (blocked layout), check it, NVT1 + eigh + VU smoothing -> f_n.
 // dk = d² of the kstore-th neighbour.
 template <int K>
 PCD_DEV void k1_epilogue(const float4* __restrict__ pos, const float4* __restrict__ nrm, int64_t N, int64_t i,
                          Vec3 vi, int (&l)[K], float dk, int k, int kstore, float rho, float tau, float damp,
-                         const Cover& cov, int32_t* __restrict__ idx, float4* __restrict__ fn, int* __restrict__ err) {
+                         const Cover& cov, int32_t* __restrict__ idx, float4* __restrict__ fn, int* __restrict__ err,
+                         const Band& band, int64_t t0) {
     bool bad = false;
 #pragma unroll
     for (int t = 0; t < K; ++t) {
@@ -180,6 +197,7 @@ PCD_DEV void k1_epilogue(const float4* __restrict__ pos, const float4* __restric
     store_list<K, true>(idx, N, i, kstore, l);   // streamed: keep L2 for the gathers
     if (bad) atomicOr(err, 1);
     if (!cov.holds(vi, dk)) atomicOr(err, 2);
+    band.mark(t0, vi, dk);
 #ifdef PCD_EXP_NONVT
     const float4 n4 = nrm[i];
     __builtin_nontemporal_store(v4f{n4.x, n4.y, n4.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
@@ -204,7 +222,7 @@ __global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __re
                                                    const float4* __restrict__ nrm, int64_t N, RowMap rm, int k,
                                                    int kstore, float rho, float tau, float damp, Cover cov,
                                                    int32_t* __restrict__ idx, float4* __restrict__ fn,
-                                                   int* __restrict__ err) {
+                                                   int* __restrict__ err, Band band) {
     const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
@@ -242,7 +260,7 @@ __global__ __launch_bounds__(256) void k_knn_nvt1(GridView g, const float4* __re
         l[t] = tk.idx(t);
         if (t == kstore - 1) dk = tk.d2(t);
     }
-    k1_epilogue<K>(pos, nrm, N, i, vi, l, dk, k, kstore, rho, tau, damp, cov, idx, fn, err);
+    k1_epilogue<K>(pos, nrm, N, i, vi, l, dk, k, kstore, rho, tau, damp, cov, idx, fn, err, band, t0);
 }
 
 // ------------------------------------------------------------------ anchored kNN (seeded iterations, K <= 32)
@@ -387,7 +405,8 @@ __global__ __launch_bounds__(kCompactBS) void k_compact_fail(const uint8_t* __re
 template <int K, bool UNIT, class P, class Nr>
 __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
                       const int32_t* __restrict__ idx, int64_t N, int64_t i, int k, int kstore, float rho, float tau,
-                      float damp, const Cover& cov, float4* __restrict__ fn, int* __restrict__ err, P rp, Nr rn) {
+                      float damp, const Cover& cov, float4* __restrict__ fn, int* __restrict__ err, P rp, Nr rn,
+                      const Band& band = Band{Cover{{1.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, nullptr}, int64_t t0 = 0) {
     const float4 p4 = pos[i];
     const Vec3 vi = v3(p4.x, p4.y, p4.z);
     int l[K];
@@ -399,12 +418,13 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
         if ((uint32_t)l[t] >= (uint32_t)N) { bad = true; l[t] = (int)i; }
     }
     if (bad) atomicOr(err, 1);
-    if (cov.enabled()) {
+    if (cov.enabled() || band.flag) {
         float dk = 0.f;
 #pragma unroll
         for (int t = 0; t < K; ++t)
             if (t == kstore - 1) dk = dist2(vi, g.pts[l[t]]);
         if (!cov.holds(vi, dk)) atomicOr(err, 2);
+        band.mark(t0, vi, dk);
     }
     // 4 neighbours in flight per batch (8 measured 0.06 ms slower at 10M: the VGPRs of 8 rows in flight)
     const Sym3 T = nvt_tensor<K, true, UNIT, 4>(rp, rn, vi, k, RegNb32{l}, rho, BlkNbSafe{idx, N, i});
@@ -430,7 +450,7 @@ __global__ __launch_bounds__(kNvtBS, PCD_NVT1_OCC) void k_nvt1(GridView g, const
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                int kstore, float rho, float tau, float damp, Cover cov,
                                                float4* __restrict__ fn, int* __restrict__ err, int win,
-                                               const uint8_t* __restrict__ skip) {
+                                               const uint8_t* __restrict__ skip, Band band) {
 #if PCD_NVT1_WIN
     __shared__ float4 s_pos[kWinRows], s_nrm[kWinRows];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
@@ -439,13 +459,14 @@ __global__ __launch_bounds__(kNvtBS, PCD_NVT1_OCC) void k_nvt1(GridView g, const
     if (t0 >= rm.nq) return;
     if (skip && skip[t0]) return;
     nvt1_row<K, UNIT>(g, pos, nrm, idx, N, rm(t0), k, kstore, rho, tau, damp, cov, fn, err, WinRows<>{pos, s_pos, lo},
-                WinRows<>{nrm, s_nrm, lo});
+                WinRows<>{nrm, s_nrm, lo}, band, t0);
 #else
     (void)win;
     const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     if (t0 >= rm.nq) return;
     if (skip && skip[t0]) return;
-    nvt1_row<K, UNIT>(g, pos, nrm, idx, N, rm(t0), k, kstore, rho, tau, damp, cov, fn, err, Rows4{pos}, Rows4{nrm});
+    nvt1_row<K, UNIT>(g, pos, nrm, idx, N, rm(t0), k, kstore, rho, tau, damp, cov, fn, err, Rows4{pos}, Rows4{nrm},
+                      band, t0);
 #endif
 }
 
@@ -523,12 +544,15 @@ template <int K>
 __global__ __launch_bounds__(kNvtBS) void k_nvt2(const float4* __restrict__ pos, const float4* __restrict__ fn,
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                float rho, float scale, uint8_t* __restrict__ cls,
-                                               float4* __restrict__ edge, int win, float4* __restrict__ probe) {
+                                               float4* __restrict__ edge, int win, float4* __restrict__ probe,
+                                               RowSel sel) {
     __shared__ float4 s_pos[WinSize<kWinHaloNvt2, kNvtBS>::rows], s_fn[WinSize<kWinHaloNvt2, kNvtBS>::rows];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
-    const int64_t lo = stage_window<kWinHaloNvt2, kNvtBS>(pos, fn, N, rm(b0), s_pos, s_fn, win);
     const int64_t t0 = b0 + threadIdx.x;
-    if (t0 >= rm.nq) return;
+    const bool mine = t0 < rm.nq && sel.take(t0);
+    if (sel.flag && !__syncthreads_or(mine)) return;     // (block-uniform: a pass skips the blocks it has no row in)
+    const int64_t lo = stage_window<kWinHaloNvt2, kNvtBS>(pos, fn, N, rm(b0), s_pos, s_fn, win);
+    if (!mine) return;
     const int64_t i = rm(t0);
     const float4 p4 = pos[i];
     // classes and the edge vector are invariant to the positive scale 1/Σw (ratios of eigenvalues, a unit
@@ -770,15 +794,18 @@ __global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, f
                                                 const int32_t* __restrict__ idx, int64_t N, RowMap rm, int ku,
                                                 const uint8_t* __restrict__ cls, int c, const float* __restrict__ g,
                                                 float d, float alpha, int win, int copy_others,
-                                                const float4* __restrict__ orig, float clampg, uint32_t moved) {
+                                                const float4* __restrict__ orig, float clampg, uint32_t moved,
+                                                RowSel sel) {
     // the flat phase moves most rows: its neighbour rows come from an LDS window of pin / fn around the block
     constexpr bool WIN = PCD_PHASE_WIN && (KIND == PCD_STEP_FLAT);
     __shared__ float4 s_pos[WIN ? WinSize<kWinHaloPhase, 256>::rows : 1], s_fn[WIN ? WinSize<kWinHaloPhase, 256>::rows : 1];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
+    const int64_t t0 = b0 + threadIdx.x;
+    const bool mine = t0 < rm.nq && sel.take(t0);
+    if (sel.flag && !__syncthreads_or(mine)) return;     // (block-uniform)
     int64_t lo = 0;
     if constexpr (WIN) lo = stage_window<kWinHaloPhase, 256>(pin, fn, N, rm(b0 < rm.nq ? b0 : rm.nq - 1), s_pos, s_fn, win);
-    const int64_t t0 = b0 + threadIdx.x;
-    if (t0 >= rm.nq) return;
+    if (!mine) return;
     const int64_t i = rm(t0);
     if (cls[i] != c) {                  // Gauss-Seidel: every phase copies the others; Jacobi / SPLIT: only the first
         if (copy_others) pout[i] = pin[i];
@@ -831,6 +858,18 @@ __global__ void k_lists(const int32_t* __restrict__ idx, const int32_t* __restri
         out[i * cols + t] = (uint32_t)j < (uint64_t)N ? (int64_t)perm[j] : -1;
     }
 }
+
+// One exchanged field of the spatial slabs (pcd_slab.h): pack reads row r from b if its class was moved by an
+// earlier phase of this iteration (the copy-free phases' two buffers), else from a; unpack writes the received row to
+// da and (non-null) db.
+struct XField {
+    const float4* a;
+    const float4* b;
+    const uint8_t* cls;
+    uint32_t moved;
+    float4* da;
+    float4* db;
+};
 
 // halo exchange: rows of one state field <-> a packed float4 buffer
 __global__ void k_pack(const float4* __restrict__ f, const int32_t* __restrict__ rows, int64_t n, float4* __restrict__ out) {
@@ -888,8 +927,32 @@ struct pcd_denoiser {
     bool timing = false;
     std::vector<hipEvent_t> ev;   // kTimingSets sets of kTimingEvents events, one set per timed iteration
     int ev_used = 0;              // sets recorded since set_timing / the last get_timing
+    // spatial slabs (pcd_slab.h): halo routes, band flags, the exchange stream and the exchange in flight
+    int npeers = 0;
+    std::vector<int> peers;
+    std::vector<int64_t> soff{0}, roff{0};   // per-peer offsets into the send / receive row lists
+    int32_t *srows = nullptr, *rrows = nullptr;
+    float4 *sbuf = nullptr, *rbuf = nullptr;  // device staging of the packed rows
+    float4 *hs = nullptr, *hr = nullptr;      // pinned host staging (host transport)
+    uint8_t* bflag = nullptr;     // per active row: its k-ball leaves the owned slab (it may read a halo row)
+    Cover own{{1.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    hipStream_t xst = nullptr;    // exchange stream
+    hipEvent_t xev_in = nullptr, xev_out = nullptr;
+    bool xpending = false;        // xev_out marks an exchange the state's next reader must wait for
+    bool xbegun = false;          // host transport: packed, callback not yet run
+    XField xfield{};
+    // CPSD driver (pcd_cpsd.h): radius lists [N][cpsd_cap] of (original index << 32 | row), member counts, overflow
+    bool nvt1_on = true;          // K1 runs NVT1 after the kNN (off: the lists only)
+    unsigned long long* ckeys = nullptr;
+    int32_t* ccnt = nullptr;
+    int* covf = nullptr;
+    int cpsd_cap = 0;
+    float4 *csave_pos = nullptr, *csave_nrm = nullptr;   // the state at the call's start (a replay after overflow)
     RowMap rowmap() const { return RowMap{rows, rows ? n_rows : n}; }
 };
+static int settle(pcd_denoiser* dn, hipStream_t st);   // (pcd_slab.h)
+static void destroy_slab_state(pcd_denoiser* dn);
+static void destroy_cpsd_state(pcd_denoiser* dn);       // (pcd_cpsd.h)
 
 #ifndef PCD_NUM_PART
 #define PCD_NUM_PART 2048
@@ -965,8 +1028,9 @@ static int select_rows(pcd_denoiser* dn, const RowMap& rm, int32_t* list, unsign
 #ifndef PCD_NVT1_OVERLAP
 #define PCD_NVT1_OVERLAP 0   // measured: the side-stream NVT1 slows the re-anchoring more than it hides
 #endif
+static const Band kNoBand{Cover{{1.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, nullptr};
 static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int K, hipStream_t st,
-                             hipEvent_t* ev) {
+                             hipEvent_t* ev, const Band& band, hipEvent_t before_nvt1) {
     const int64_t N = dn->n;
     const RowMap rm = dn->rowmap();
     const int kstore = std::max(p->k, p->k_update);
@@ -1020,7 +1084,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
                 PCD_HIP(hipEventRecord(dn->fork, st));                                                                 \
                 PCD_HIP(hipStreamWaitEvent(dn->side, dn->fork, 0));                                                    \
                 hipLaunchKernelGGL((k_nvt1<C, false>), grd_nvt, blk_nvt, 0, dn->side, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,   \
-                                   p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, dn->fail);          \
+                                   p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, dn->fail, kNoBand); \
                 PCD_HIP(hipEventRecord(dn->join, dn->side));                                                           \
             }                                                                                                          \
             if (ev) PCD_HIP(hipEventRecord(ev[1], st));                                                                \
@@ -1031,16 +1095,19 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
         hipLaunchKernelGGL((k_knn_redo_wave<2 * C, false>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,       \
                            dn->alist, dn->idx, dn->spill, spill_cnt, dn->err);                                         \
         if (ev) PCD_HIP(hipEventRecord(ev[3], st));                                                                    \
+        if (before_nvt1) PCD_HIP(hipStreamWaitEvent(st, before_nvt1, 0));                                              \
         if (overlap) {                                                                                                 \
             hipLaunchKernelGGL((k_nvt1_list<C>), grd_list, blk, 0, st, gv, P, dn->nrm, dn->idx, N, p->k, kstore,       \
                                p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->redo, redo_cnt);                 \
             PCD_HIP(hipStreamWaitEvent(st, dn->join, 0));                                                              \
+        } else if (!dn->nvt1_on) {                                                                                     \
+            /* the kNN lists only (the CPSD driver's update selection, pcd_cpsd.h) */                                   \
         } else if (dn->unit_nrm) {                                                                                     \
             hipLaunchKernelGGL((k_nvt1<C, true>), grd_nvt, blk_nvt, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,       \
-                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, nullptr);               \
+                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, nullptr, band);         \
         } else {                                                                                                       \
             hipLaunchKernelGGL((k_nvt1<C, false>), grd_nvt, blk_nvt, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,      \
-                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, nullptr);               \
+                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, nullptr, band);         \
         }                                                                                                              \
         break;
     switch (K) {
@@ -1054,14 +1121,19 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     return PCD_OK;
 }
 
-static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t st, hipEvent_t* ev = nullptr) {
+// band: spatial slabs, mark the rows that may read a halo row (pcd_slab_iterate); before_nvt1: an event the
+// neighbour gathers must wait for (the previous iteration's position exchange; the kNN itself reads only the row's
+// own position and the frozen snapshot).
+static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t st, hipEvent_t* ev = nullptr,
+                    const Band& band = kNoBand, hipEvent_t before_nvt1 = nullptr) {
     const int64_t N = dn->n;
     const RowMap rm = dn->rowmap();
     const int kstore = std::max(p->k, p->k_update);
     const int K = list_cap(p);
     if (rm.nq > 0 && dn->seeding && dn->anchoring && K <= 32 && N >= 2 * K && knn_cap(dn->kcap) <= 32)
-        return stage_k1_anchored(dn, p, K, st, ev);
+        return stage_k1_anchored(dn, p, K, st, ev, band, before_nvt1);
     if (ev) for (int e = 1; e <= 3; ++e) PCD_HIP(hipEventRecord(ev[e], st));   // no anchored sub-stages
+    if (before_nvt1) PCD_HIP(hipStreamWaitEvent(st, before_nvt1, 0));         // (the fused kernel gathers at once)
     if (rm.nq == 0) return PCD_OK;
     const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
     const GridView gv = dn->g->view;
@@ -1069,8 +1141,8 @@ static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t s
     const bool seed = dn->seeding && dn->seed_cols >= kstore;
 #define PCD_K1(C)                                                                                                      \
     case C:                                                                                                            \
-        if (seed) hipLaunchKernelGGL((k_knn_nvt1<C, true>), grd, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore, p->rho, p->tau, p->damp, dn->cov, dn->idx, dn->fn, dn->err); \
-        else hipLaunchKernelGGL((k_knn_nvt1<C, false>), grd, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore, p->rho, p->tau, p->damp, dn->cov, dn->idx, dn->fn, dn->err); \
+        if (seed) hipLaunchKernelGGL((k_knn_nvt1<C, true>), grd, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore, p->rho, p->tau, p->damp, dn->cov, dn->idx, dn->fn, dn->err, band); \
+        else hipLaunchKernelGGL((k_knn_nvt1<C, false>), grd, blk, 0, st, gv, P, dn->nrm, N, rm, p->k, kstore, p->rho, p->tau, p->damp, dn->cov, dn->idx, dn->fn, dn->err, band); \
         break;
     switch (K) {
         PCD_K1(8) PCD_K1(16) PCD_K1(32) PCD_K1(64)
@@ -1082,14 +1154,14 @@ static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t s
     return PCD_OK;
 }
 
-static int stage_k2(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t st) {
+static int stage_k2(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t st, RowSel sel = RowSel{nullptr, 0}) {
     const RowMap rm = dn->rowmap();
     if (rm.nq == 0) return PCD_OK;
     const dim3 blk(kNvtBS), grd((unsigned)cdiv(rm.nq, kNvtBS));
     float4* P = dn->pos[dn->cur];
 #define PCD_K2(C) \
     case C:                                                                                                            \
-        hipLaunchKernelGGL((k_nvt2<C>), grd, blk, 0, st, P, dn->fn, dn->idx, dn->n, rm, p->k, p->rho, p->class_scale, dn->cls, dn->edge, dn->windows, dn->probe); \
+        hipLaunchKernelGGL((k_nvt2<C>), grd, blk, 0, st, P, dn->fn, dn->idx, dn->n, rm, p->k, p->rho, p->class_scale, dn->cls, dn->edge, dn->windows, dn->probe, sel); \
         break;
     switch (list_cap(p)) {
         PCD_K2(8) PCD_K2(16) PCD_K2(32) PCD_K2(64)
@@ -1149,8 +1221,10 @@ static int stage_maxdist(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, 
 
 // split: the fused loop's copy-free phases (k_phase SPLIT; pcd_denoiser_iterate decides), moved = the classes the
 // earlier phases of this iteration moved into pos[cur ^ 1]; cur flips after the last phase only.
+// sel: one pass of the rows (spatial slabs: the rows that read no halo row, then the others after the exchange);
+// flip: this call completes the phase (the last pass), cur may flip.
 static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, const float* red1, hipStream_t st,
-                       bool split = false, uint32_t moved = 0) {
+                       bool split = false, uint32_t moved = 0, RowSel sel = RowSel{nullptr, 0}, bool flip = true) {
     const RowMap rm = dn->rowmap();
     dn->part_ph = dn->scan_ph = -1;     // positions change: the partials' boxes no longer describe them
     float* gs = dn->gscal + 4 * ph;
@@ -1162,7 +1236,7 @@ static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, co
     const int copy_others = split ? 0 : (!p->jacobi || ph == 0) ? 1 : 0;
     if (rm.nq > 0) {
         const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
-#define PCD_PH2(KD, C) hipLaunchKernelGGL((k_phase<KD, C>), grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, dn->n, rm, p->k_update, dn->cls, c, gs, p->d, a, dn->windows, copy_others, dn->orig, p->clamp_global, moved)
+#define PCD_PH2(KD, C) hipLaunchKernelGGL((k_phase<KD, C>), grd, blk, 0, st, pin, pout, dn->fn, dn->edge, dn->idx, dn->n, rm, p->k_update, dn->cls, c, gs, p->d, a, dn->windows, copy_others, dn->orig, p->clamp_global, moved, sel)
 #define PCD_PH(KD)                                                                                                     \
     switch (knn_cap(p->k_update)) {                                                                                    \
         case 8: PCD_PH2(KD, 8); break;                                                                                 \
@@ -1182,7 +1256,7 @@ static int stage_apply(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, co
 #undef PCD_PH2
         PCD_LAUNCH_CHECK();
     }
-    if (split ? ph == p->nphases - 1 : !p->jacobi) dn->cur ^= 1;   // Jacobi: the swap happens at finish
+    if (flip && (split ? ph == p->nphases - 1 : !p->jacobi)) dn->cur ^= 1;   // Jacobi: the swap happens at finish
     return PCD_OK;
 }
 
@@ -1198,6 +1272,7 @@ static float4* field_ptr(pcd_denoiser* dn, int field) {
         case PCD_FIELD_POS: return dn->pos[dn->cur];
         case PCD_FIELD_NRM: return dn->nrm;
         case PCD_FIELD_FN: return dn->fn;
+        case PCD_FIELD_EDGE: return dn->edge;
         default: return nullptr;
     }
 }
@@ -1240,6 +1315,8 @@ int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out) {
 
 int pcd_denoiser_destroy(pcd_denoiser* dn) {
     if (!dn) return PCD_OK;
+    destroy_slab_state(dn);
+    destroy_cpsd_state(dn);
     (void)hipFree(dn->pos[0]); (void)hipFree(dn->pos[1]); (void)hipFree(dn->nrm); (void)hipFree(dn->fn);
     (void)hipFree(dn->edge); (void)hipFree(dn->orig); (void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part);
     (void)hipFree(dn->red); (void)hipFree(dn->gscal); (void)hipFree(dn->err);
@@ -1255,6 +1332,7 @@ int pcd_denoiser_destroy(pcd_denoiser* dn) {
 
 int pcd_denoiser_load(pcd_denoiser* dn, const float* pos, const float* n, void* stream) {
     PCD_CHECK_ARG(dn && pos && n, "null argument");
+    if (settle(dn, as_stream(stream)) != PCD_OK) return PCD_ERR_HIP;
     hipLaunchKernelGGL(k_load, dim3((unsigned)cdiv(dn->n, 256)), dim3(256), 0, as_stream(stream), pos, n,
                        dn->g->perm, dn->n, dn->pos[0], dn->nrm, dn->orig);
     PCD_LAUNCH_CHECK();
@@ -1296,6 +1374,7 @@ int pcd_denoiser_pack(pcd_denoiser* dn, int field, const int32_t* rows, int64_t 
     float4* f = field_ptr(dn, field);
     PCD_CHECK_ARG(f != nullptr, "bad field");
     PCD_CHECK_ARG(n == 0 || (rows && out4), "null rows / buffer");
+    if (settle(dn, as_stream(stream)) != PCD_OK) return PCD_ERR_HIP;
     if (n == 0) return PCD_OK;
     hipLaunchKernelGGL(k_pack, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, as_stream(stream), f, rows, n,
                        reinterpret_cast<float4*>(out4));
@@ -1308,6 +1387,7 @@ int pcd_denoiser_unpack(pcd_denoiser* dn, int field, const int32_t* rows, int64_
     float4* f = field_ptr(dn, field);
     PCD_CHECK_ARG(f != nullptr, "bad field");
     PCD_CHECK_ARG(n == 0 || (rows && in4), "null rows / buffer");
+    if (settle(dn, as_stream(stream)) != PCD_OK) return PCD_ERR_HIP;
     if (n == 0) return PCD_OK;
     dn->part_ph = dn->scan_ph = -1;
     hipLaunchKernelGGL(k_unpack, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, as_stream(stream), f, rows, n,
@@ -1326,6 +1406,7 @@ int pcd_denoiser_stage(pcd_denoiser* dn, const pcd_denoise_params* p, int stage,
     PCD_CHECK_ARG(!ph_stage || (phase >= 0 && phase < p->nphases), "phase out of range");
     PCD_CHECK_ARG(!(stage == PCD_STAGE_PHASE_SUM || stage == PCD_STAGE_PHASE_CENTRE) || red, "red is null");
     hipStream_t st = as_stream(stream);
+    if (settle(dn, st) != PCD_OK) return PCD_ERR_HIP;
     switch (stage) {
         case PCD_STAGE_KNN_NVT1: return stage_k1(dn, p, st);
         case PCD_STAGE_NVT2: return stage_k2(dn, p, st);
@@ -1358,6 +1439,7 @@ int pcd_denoiser_status(pcd_denoiser* dn, int* bits, void* stream) {
 int pcd_denoiser_lists(pcd_denoiser* dn, int64_t* out, int cols, void* stream) {
     PCD_CHECK_ARG(dn && out, "null argument");
     PCD_CHECK_ARG(dn->iterated && cols >= 1 && cols <= dn->list_cols, "cols must be in [1, stored list length]");
+    if (settle(dn, as_stream(stream)) != PCD_OK) return PCD_ERR_HIP;
     hipLaunchKernelGGL(k_lists, dim3((unsigned)cdiv(dn->n, 256)), dim3(256), 0, as_stream(stream), dn->idx,
                        dn->g->perm, dn->n, cols, out);
     PCD_LAUNCH_CHECK();
@@ -1433,6 +1515,7 @@ int pcd_denoiser_set_probe(pcd_denoiser* dn, int enable) {
 int pcd_denoiser_probe_store(pcd_denoiser* dn, float* nvt2_eig4, void* stream) {
     PCD_CHECK_ARG(dn && nvt2_eig4, "null argument");
     PCD_CHECK_ARG(dn->probe != nullptr, "probe not enabled (pcd_denoiser_set_probe)");
+    if (settle(dn, as_stream(stream)) != PCD_OK) return PCD_ERR_HIP;
     hipLaunchKernelGGL(k_scatter4, dim3((unsigned)cdiv(dn->n, 256)), dim3(256), 0, as_stream(stream), dn->probe,
                        dn->g->perm, dn->n, reinterpret_cast<float4*>(nvt2_eig4));
     PCD_LAUNCH_CHECK();
@@ -1482,6 +1565,7 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
     int rc = check_params(dn, p);
     if (rc != PCD_OK) return rc;
     hipStream_t st = as_stream(stream);
+    if ((rc = settle(dn, st)) != PCD_OK) return rc;
     for (int it = 0; it < iterations; ++it) {
         hipEvent_t* ev = nullptr;     // this iteration's event set (timing on, and a set left)
         if (dn->timing && dn->ev_used < kTimingSets) ev = &dn->ev[(size_t)dn->ev_used++ * kTimingEvents];
@@ -1521,6 +1605,7 @@ int pcd_denoiser_store(pcd_denoiser* dn, float* pos, float* n, int64_t* classes,
     PCD_CHECK_ARG(dn != nullptr, "null denoiser");
     PCD_CHECK_ARG(dn->loaded, "nothing loaded");
     PCD_CHECK_ARG(dn->iterated || (!classes && !edge_vectors), "classes/edge vectors need one iteration");
+    if (settle(dn, as_stream(stream)) != PCD_OK) return PCD_ERR_HIP;
     hipLaunchKernelGGL(k_store, dim3((unsigned)cdiv(dn->n, 256)), dim3(256), 0, as_stream(stream), dn->pos[dn->cur],
                        dn->nrm, dn->cls, dn->edge, dn->g->perm, dn->n, pos, n, classes, edge_vectors);
     PCD_LAUNCH_CHECK();
@@ -1528,3 +1613,6 @@ int pcd_denoiser_store(pcd_denoiser* dn, float* pos, float* n, int64_t* classes,
 }
 
 }  // extern "C"
+
+#include "pcd_slab.h"
+#include "pcd_cpsd.h"

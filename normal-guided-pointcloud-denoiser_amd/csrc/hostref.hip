@@ -54,6 +54,22 @@ int pcd_host_solve3(const float* a9, const float* b3, int64_t m, float* x3, int3
     return PCD_OK;
 }
 
+int pcd_host_inv3(const float* a9, int64_t m, float* inv9, int32_t* ok) {
+    PCD_CHECK_ARG(a9 && inv9 && ok, "null argument");
+    for (int64_t i = 0; i < m; ++i) {
+        float A[3][3], X[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) A[r][c] = a9[9 * i + 3 * r + c];
+        ok[i] = inv3_ref(A, X) ? 1 : 0;
+        if (!ok[i])
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) X[r][c] = 0.f;
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) inv9[9 * i + 3 * r + c] = X[r][c];
+    }
+    return PCD_OK;
+}
+
 int pcd_host_nvt_tensor(const float* pos, const float* n, const int64_t* ci, const int64_t* off, const int64_t* nbr,
                         int64_t m, float rho, float* t6) {
     PCD_CHECK_ARG(pos && n && ci && off && (m == 0 || nbr) && t6, "null argument");

@@ -131,11 +131,12 @@ extern "C" int pcd_mesh_vta(const void* f, int f_bits, int64_t nf, int64_t nv, v
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
     const size_t n = (size_t)std::max<int64_t>(nc, 1);
-    PCD_HIP(hipMallocAsync((void**)&keys, n * 4, st));
-    PCD_HIP(hipMallocAsync((void**)&vals, n * 4, st));
-    PCD_HIP(hipMallocAsync((void**)&skeys, n * 4, st));
-    PCD_HIP(hipMallocAsync((void**)&svals, n * 4, st));
-    PCD_HIP(hipMallocAsync((void**)&bad, sizeof(int), st));
+    StreamTemps tt(st);                    // freed on every exit path
+    PCD_HIP(tt.alloc(&keys, n * 4));
+    PCD_HIP(tt.alloc(&vals, n * 4));
+    PCD_HIP(tt.alloc(&skeys, n * 4));
+    PCD_HIP(tt.alloc(&svals, n * 4));
+    PCD_HIP(tt.alloc(&bad, sizeof(int)));
     PCD_HIP(hipMemsetAsync(bad, 0, sizeof(int), st));
     const dim3 blk(256);
     if (nc > 0) {
@@ -144,7 +145,7 @@ extern "C" int pcd_mesh_vta(const void* f, int f_bits, int64_t nf, int64_t nv, v
         unsigned end_bit = 1;
         while (end_bit < 32 && ((uint64_t)1 << end_bit) < (uint64_t)nv) ++end_bit;
         (void)rocprim::radix_sort_pairs(nullptr, tmp_bytes, keys, skeys, vals, svals, (size_t)nc, 0u, end_bit, st);
-        PCD_HIP(hipMallocAsync(&tmp, tmp_bytes, st));
+        PCD_HIP(tt.alloc(&tmp, tmp_bytes));
         if (rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, skeys, vals, svals, (size_t)nc, 0u, end_bit, st) != hipSuccess)
             return fail(PCD_ERR_HIP, "pcd_mesh_vta: rocprim::radix_sort_pairs failed");
     }
@@ -154,10 +155,7 @@ extern "C" int pcd_mesh_vta(const void* f, int f_bits, int64_t nf, int64_t nv, v
     PCD_LAUNCH_CHECK();
     int hbad = 0;
     PCD_HIP(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, st));
-    PCD_HIP(hipFreeAsync(keys, st)); PCD_HIP(hipFreeAsync(vals, st)); PCD_HIP(hipFreeAsync(skeys, st));
-    PCD_HIP(hipFreeAsync(svals, st)); PCD_HIP(hipFreeAsync(bad, st));
-    if (tmp) PCD_HIP(hipFreeAsync(tmp, st));
-    PCD_HIP(hipStreamSynchronize(st));
+    PCD_HIP(tt.release());                 // (synchronises: hbad is valid)
     PCD_CHECK_ARG(hbad == 0, "face index out of range [0, nv)");
     return PCD_OK;
 }
@@ -171,10 +169,11 @@ extern "C" int pcd_mesh_update_f32(float* v, int64_t nv, const int32_t* f, const
     hipStream_t st = as_stream(stream);
     float4 *a = nullptr, *b = nullptr, *fn4 = nullptr;
     int4* f4 = nullptr;
-    PCD_HIP(hipMallocAsync((void**)&a, nv * sizeof(float4), st));
-    PCD_HIP(hipMallocAsync((void**)&b, nv * sizeof(float4), st));
-    PCD_HIP(hipMallocAsync((void**)&fn4, nf * sizeof(float4), st));
-    PCD_HIP(hipMallocAsync((void**)&f4, nf * sizeof(int4), st));
+    StreamTemps tt(st);                    // freed on every exit path
+    PCD_HIP(tt.alloc(&a, nv * sizeof(float4)));
+    PCD_HIP(tt.alloc(&b, nv * sizeof(float4)));
+    PCD_HIP(tt.alloc(&fn4, nf * sizeof(float4)));
+    PCD_HIP(tt.alloc(&f4, nf * sizeof(int4)));
     const dim3 blk(256);
     hipLaunchKernelGGL(k_rows3_to4, dim3((unsigned)cdiv(nv, 256)), blk, 0, st, v, nv, a);
     hipLaunchKernelGGL(k_rows3_to4, dim3((unsigned)cdiv(nf, 256)), blk, 0, st, fn, nf, fn4);
@@ -188,7 +187,7 @@ extern "C" int pcd_mesh_update_f32(float* v, int64_t nv, const int32_t* f, const
     }
     hipLaunchKernelGGL(k_rows4_to3, dim3((unsigned)cdiv(nv, 256)), blk, 0, st, buf[cur], nv, v);
     PCD_LAUNCH_CHECK();
-    PCD_HIP(hipFreeAsync(a, st)); PCD_HIP(hipFreeAsync(b, st)); PCD_HIP(hipFreeAsync(fn4, st)); PCD_HIP(hipFreeAsync(f4, st));
+    PCD_HIP(tt.release(false));
     return PCD_OK;
 }
 
@@ -199,7 +198,8 @@ extern "C" int pcd_mesh_update(double* v, int64_t nv, const int64_t* f, const do
     PCD_CHECK_ARG(v && f && fn && vf && ni && nf > 0, "null argument");
     hipStream_t st = as_stream(stream);
     double* tmp = nullptr;
-    PCD_HIP(hipMallocAsync((void**)&tmp, nv * 3 * sizeof(double), st));
+    StreamTemps tt(st);                    // freed on every exit path
+    PCD_HIP(tt.alloc(&tmp, nv * 3 * sizeof(double)));
     double* buf[2] = {v, tmp};
     int cur = 0;
     const dim3 grd((unsigned)cdiv(nv, 256)), blk(256);
@@ -209,6 +209,6 @@ extern "C" int pcd_mesh_update(double* v, int64_t nv, const int64_t* f, const do
     }
     PCD_LAUNCH_CHECK();
     if (cur != 0) PCD_HIP(hipMemcpyAsync(v, tmp, nv * 3 * sizeof(double), hipMemcpyDeviceToDevice, st));
-    PCD_HIP(hipFreeAsync(tmp, st));
+    PCD_HIP(tt.release(false));
     return PCD_OK;
 }

@@ -1,0 +1,213 @@
+// The CPSD ("Martin") comparison driver fused on the device: PostProcessing.ipynb:1041-1062, the
+// thesis' 50-iteration baseline, as one library call.  Included once at the end of denoise.hip (it drives the fused
+// loop's static stages).
+//
+// Per iteration, every step on the stream, no host synchronisation:
+//   kNN(k_u) of the current positions            the fused loop's anchored kNN, lists only (Selector.py:235-246)
+//   k_cpsd_nvt  radius selection r of the current positions over the frozen snapshot (Selector.py:214-233: scipy's
+//               f64 membership, members in ascending ORIGINAL index), normal-filtered NVT (Decompositionor.py:260-276),
+//               LAPACK-restated eigh, VU smoothing (:92-106) -> f_n
+//   k_cpsd_pvt  normal-filtered PVT on f_n over the same members (:172-211), eigh, VU features (eigval < tau).sum % 3
+//               (:84-85) -> classes, smallest eigenvector -> edge vectors
+//   phases      flat_step (global centre / delta) / edge_step / corner_step with alphas, Jacobi across classes
+//               (temp_pos = pos.clone()), per-step clamp d * 20000, global clamp ||temp_pos - original_pos|| < d
+//               (the fused loop's jacobi + clamp_global phases, Denoiser.py:26-119)
+//   n := f_n
+// Radius lists live in [N][cap] slots of 64-bit keys (original index << 32 | snapshot row), sorted per row in place.
+// A row with more than cap members raises a device flag; the call checks it once at the end (its only host sync) and,
+// if set, restores the state it started from, doubles cap and runs again -- results never depend on cap.
+
+namespace pcd {
+
+static constexpr int kCpsdBS = 128;
+
+// Members of row i's list in ascending original index (the keys' row halves).
+struct KeyNb {
+    const unsigned long long* L;
+    PCD_DEV int64_t operator()(int t) const { return (int64_t)(uint32_t)(L[t] & 0xFFFFFFFFull); }
+};
+
+// Radius selection + normal-filtered NVT + VU smoothing of each active row.
+__global__ __launch_bounds__(kCpsdBS) void k_cpsd_nvt(GridView g, const float4* __restrict__ pos,
+                                                      const float4* __restrict__ nrm, int64_t N, RowMap rm, float r,
+                                                      float rho, float tau, float damp,
+                                                      unsigned long long* __restrict__ keys, int cap,
+                                                      int32_t* __restrict__ cnt, float4* __restrict__ fn,
+                                                      int* __restrict__ ovf) {
+    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * kCpsdBS + threadIdx.x;
+    if (t0 >= rm.nq) return;
+    const int64_t i = rm(t0);
+    const float4 q4 = pos[i];
+    const float qx = q4.x, qy = q4.y, qz = q4.z;
+    unsigned long long* L = keys + (size_t)i * (size_t)cap;
+    int m = 0;
+    const double rd = (double)r, r2 = rd * rd;
+    if (rd >= 0.0) {
+        // the cells overlapping [q - r, q + r] (an f32 box widened by a ulp-scale margin); membership is scipy's f64
+        // ((dx² + dy²) + dz²) <= r² on the exact f32 inputs (k_radius, pcd_radius_count / _fill)
+        const float rf = (float)(rd * (1.0 + 1e-6)) + 1e-30f;
+        const int lo[3] = {max(cell_coord(qx - rf, g.ox, g.inv_h), 0), max(cell_coord(qy - rf, g.oy, g.inv_h), 0),
+                           max(cell_coord(qz - rf, g.oz, g.inv_h), 0)};
+        const int hi[3] = {min(cell_coord(qx + rf, g.ox, g.inv_h), g.dx - 1),
+                           min(cell_coord(qy + rf, g.oy, g.inv_h), g.dy - 1),
+                           min(cell_coord(qz + rf, g.oz, g.inv_h), g.dz - 1)};
+        for (int cz = lo[2]; cz <= hi[2]; ++cz)
+            for (int cy = lo[1]; cy <= hi[1]; ++cy)
+                for (int cx = lo[0]; cx <= hi[0]; ++cx) {
+                    uint32_t s, e;
+                    if (!cell_range(g, cx, cy, cz, s, e)) continue;
+                    for (uint32_t r0 = s; r0 < e; ++r0) {
+                        const float4 p = g.pts[r0];
+                        const double dx = (double)qx - (double)p.x, dy = (double)qy - (double)p.y,
+                                     dz = (double)qz - (double)p.z;
+                        const double d2 = __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
+                        if (d2 <= r2) {
+                            if (m < cap) L[m] = ((unsigned long long)__float_as_uint(p.w) << 32) | r0;
+                            ++m;
+                        }
+                    }
+                }
+    }
+    cnt[i] = m;
+    if (m > cap) {          // (the call replays with a larger cap; this row's result is discarded)
+        atomicOr(ovf, 1);
+        m = cap;
+    }
+    // ascending original index: scipy's per-query order, the order the reference's scatter sums in
+    for (int a = 1; a < m; ++a) {
+        const unsigned long long k = L[a];
+        int b = a - 1;
+        while (b >= 0 && L[b] > k) { L[b + 1] = L[b]; --b; }
+        L[b + 1] = k;
+    }
+    const float4 n4 = nrm[i];
+    const Vec3 ni = v3(n4.x, n4.y, n4.z);
+    const Sym3 T = nvt_normal_tensor(Rows4{nrm}, ni, m, KeyNb{L}, rho);
+    float w[3], V[3][3];
+    eigh3(T, w, V);
+    const Vec3 f = vu_smooth(w, V, ni, tau, damp);
+    fn[i] = make_float4(f.x, f.y, f.z, 0.f);
+}
+
+// Normal-filtered PVT on f_n over the same members, eigh, VU features + edge vector of each active row.
+__global__ __launch_bounds__(kCpsdBS) void k_cpsd_pvt(const float4* __restrict__ pos, const float4* __restrict__ fn,
+                                                      int64_t N, RowMap rm, float rho, float tau,
+                                                      const unsigned long long* __restrict__ keys, int cap,
+                                                      const int32_t* __restrict__ cnt, uint8_t* __restrict__ cls,
+                                                      float4* __restrict__ edge) {
+    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * kCpsdBS + threadIdx.x;
+    if (t0 >= rm.nq) return;
+    const int64_t i = rm(t0);
+    const int m = min(cnt[i], cap);
+    const float4 p4 = pos[i], f4 = fn[i];
+    const Sym3 C = pvt_normal_cov(Rows4{pos}, Rows4{fn}, v3(p4.x, p4.y, p4.z), v3(f4.x, f4.y, f4.z), m,
+                                  KeyNb{keys + (size_t)i * (size_t)cap}, rho);
+    float w[3], V[3][3];
+    eigh3(C, w, V);
+    // getVUFeatures(tau) = (eigval < tau).sum(dim=1) % 3 (Decompositionor.py:84-85); NaN compares false
+    const int below = (w[0] < tau ? 1 : 0) + (w[1] < tau ? 1 : 0) + (w[2] < tau ? 1 : 0);
+    cls[i] = (uint8_t)(below % 3);
+    edge[i] = make_float4(V[0][0], V[1][0], V[2][0], 0.f);   // eigvec[..., 0] (Processor's edge_vectors)
+}
+
+}  // namespace pcd
+
+static void destroy_cpsd_state(pcd_denoiser* dn) {
+    (void)hipFree(dn->ckeys); (void)hipFree(dn->ccnt); (void)hipFree(dn->covf);
+    (void)hipFree(dn->csave_pos); (void)hipFree(dn->csave_nrm);
+    dn->ckeys = nullptr; dn->ccnt = nullptr; dn->covf = nullptr;
+    dn->csave_pos = dn->csave_nrm = nullptr;
+    dn->cpsd_cap = 0;
+}
+
+static int cpsd_alloc(pcd_denoiser* dn, int cap) {
+    const int64_t N = dn->n;
+    (void)hipFree(dn->ckeys);
+    dn->ckeys = nullptr;
+    dn->cpsd_cap = 0;
+    if (hipMalloc(&dn->ckeys, (size_t)N * (size_t)cap * sizeof(unsigned long long)) != hipSuccess)
+        return fail(PCD_ERR_OOM, "pcd_cpsd_iterate: radius lists");
+    if (!dn->ccnt && (hipMalloc(&dn->ccnt, N * sizeof(int32_t)) != hipSuccess ||
+                      hipMalloc(&dn->covf, sizeof(int)) != hipSuccess ||
+                      hipMalloc(&dn->csave_pos, N * sizeof(float4)) != hipSuccess ||
+                      hipMalloc(&dn->csave_nrm, N * sizeof(float4)) != hipSuccess))
+        return fail(PCD_ERR_OOM, "pcd_cpsd_iterate: buffers");
+    dn->cpsd_cap = cap;
+    return PCD_OK;
+}
+
+extern "C" {
+
+int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations, void* stream) {
+    PCD_CHECK_ARG(dn && cp, "null argument");
+    PCD_CHECK_ARG(dn->loaded, "pcd_denoiser_load must be called first");
+    PCD_CHECK_ARG(iterations >= 0, "iterations must be >= 0");
+    PCD_CHECK_ARG(cp->k_update >= 1 && cp->k_update <= dn->kcap && cp->k_update <= dn->n, "k_update out of range");
+    PCD_CHECK_ARG(!(cp->r < 0.f) && !(cp->d < 0.f) && !(cp->step_clamp < 0.f), "r, d, step_clamp must be >= 0");
+    hipStream_t st = as_stream(stream);
+    int rc = settle(dn, st);
+    if (rc != PCD_OK) return rc;
+    // the fused loop's parameters for the kNN lists and the phases: Jacobi across classes with the global clamp
+    pcd_denoise_params p{};
+    p.k = p.k_update = cp->k_update;
+    p.rho = cp->rho; p.tau = cp->tau; p.damp = cp->damp; p.class_scale = 0.2f;
+    p.d = cp->step_clamp;
+    p.nphases = 3;
+    const int kinds[3] = {PCD_STEP_FLAT, PCD_STEP_EDGE, PCD_STEP_CORNER};
+    for (int ph = 0; ph < 3; ++ph) { p.phase_class[ph] = ph; p.phase_kind[ph] = kinds[ph]; p.phase_alpha[ph] = cp->alpha[ph]; }
+    p.jacobi = 1;
+    p.clamp_global = cp->d;
+    if ((rc = check_params(dn, &p)) != PCD_OK) return rc;
+    if (dn->cpsd_cap == 0 && (rc = cpsd_alloc(dn, 32)) != PCD_OK) return rc;
+    const int64_t N = dn->n;
+    const RowMap rm = dn->rowmap();
+    // the state this call starts from (a replay after a radius-list overflow restarts from it)
+    PCD_HIP(hipMemcpyAsync(dn->csave_pos, dn->pos[dn->cur], N * sizeof(float4), hipMemcpyDeviceToDevice, st));
+    PCD_HIP(hipMemcpyAsync(dn->csave_nrm, dn->nrm, N * sizeof(float4), hipMemcpyDeviceToDevice, st));
+    const int cur0 = dn->cur;
+    const bool unit0 = dn->unit_nrm;
+    for (int attempt = 0;; ++attempt) {
+        PCD_HIP(hipMemsetAsync(dn->covf, 0, sizeof(int), st));
+        dn->nvt1_on = false;
+        for (int it = 0; it < iterations && rc == PCD_OK; ++it) {
+            rc = stage_k1(dn, &p, st);                         // kNN(k_u) lists of the current positions
+            if (rc != PCD_OK) break;
+            const GridView gv = dn->g->view;
+            const dim3 grd((unsigned)cdiv(rm.nq, kCpsdBS)), blk(kCpsdBS);
+            if (rm.nq > 0) {
+                hipLaunchKernelGGL(k_cpsd_nvt, grd, blk, 0, st, gv, dn->pos[dn->cur], dn->nrm, N, rm, cp->r, cp->rho,
+                                   cp->tau, cp->damp, dn->ckeys, dn->cpsd_cap, dn->ccnt, dn->fn, dn->covf);
+                hipLaunchKernelGGL(k_cpsd_pvt, grd, blk, 0, st, dn->pos[dn->cur], dn->fn, N, rm, cp->rho, cp->tau,
+                                   dn->ckeys, dn->cpsd_cap, dn->ccnt, dn->cls, dn->edge);
+                if (hipGetLastError() != hipSuccess) { rc = fail(PCD_ERR_HIP, "pcd_cpsd_iterate: launch"); break; }
+            }
+            for (int ph = 0; ph < 3 && rc == PCD_OK; ++ph) {
+                if (phase_is_global(&p, ph)) {
+                    double* red4 = dn->red + 4 * ph;
+                    if ((rc = stage_sum(dn, &p, ph, red4, st)) != PCD_OK) break;
+                    if ((rc = stage_centre(dn, ph, red4, st)) != PCD_OK) break;
+                    if ((rc = stage_maxdist(dn, &p, ph, nullptr, st)) != PCD_OK) break;
+                }
+                rc = stage_apply(dn, &p, ph, nullptr, st);
+            }
+            if (rc == PCD_OK) stage_finish(dn, &p);
+        }
+        dn->nvt1_on = true;
+        if (rc != PCD_OK) return rc;
+        int ovf = 0;
+        PCD_HIP(hipMemcpyAsync(&ovf, dn->covf, sizeof(int), hipMemcpyDeviceToHost, st));
+        PCD_HIP(hipStreamSynchronize(st));
+        if (!ovf || iterations == 0) break;
+        // a radius selection had more members than the list slots: restart from the saved state with twice the slots
+        const int cap = dn->cpsd_cap * 2;
+        PCD_CHECK_ARG(attempt < 12 && (int64_t)cap * N < (1ll << 33), "radius selections too large for the device lists");
+        if ((rc = cpsd_alloc(dn, cap)) != PCD_OK) return rc;
+        dn->cur = cur0;
+        PCD_HIP(hipMemcpyAsync(dn->pos[dn->cur], dn->csave_pos, N * sizeof(float4), hipMemcpyDeviceToDevice, st));
+        PCD_HIP(hipMemcpyAsync(dn->nrm, dn->csave_nrm, N * sizeof(float4), hipMemcpyDeviceToDevice, st));
+        dn->unit_nrm = unit0;
+    }
+    return PCD_OK;
+}
+
+}  // extern "C"

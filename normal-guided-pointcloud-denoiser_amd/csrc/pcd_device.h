@@ -549,39 +549,82 @@ PCD_DEV void eigh3(Sym3 A, float w[3], float V[3][3]) {
         for (int k = 0; k < 3; ++k) V[r][k] = Z[r][k];
 }
 
-// ---------------------------------------------------------------- 3x3 general solve
-// LU with partial pivoting (first max |a| wins, as LAPACK i*amax).  Returns false iff a pivot is exactly
-// zero -- the condition under which torch.linalg.inv_ex reports info != 0.
-PCD_DEV bool solve3(float A[3][3], Vec3 bv, Vec3& x) {
-    float b[3] = {bv.x, bv.y, bv.z};
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        int piv = c;
-        float best = fabsf(A[c][c]);
-#pragma unroll
-        for (int r = c + 1; r < 3; ++r) {
-            const float v = fabsf(A[r][c]);
-            if (v > best) { best = v; piv = r; }
-        }
-        if (A[piv][c] == 0.f) return false;
-        if (piv != c) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) { float t = A[c][k]; A[c][k] = A[piv][k]; A[piv][k] = t; }
-            float t = b[c]; b[c] = b[piv]; b[piv] = t;
-        }
-        const float inv = 1.f / A[c][c];
-#pragma unroll
-        for (int r = c + 1; r < 3; ++r) {
-            const float f = A[r][c] * inv;
-#pragma unroll
-            for (int k = c; k < 3; ++k) A[r][k] -= f * A[c][k];
-            b[r] -= f * b[c];
-        }
+// ---------------------------------------------------------------- 3x3 inverse, then A^-1 b (the reference's order)
+// The position steps call torch.linalg.inv_ex(A) and then einsum("nij,nj->ni", A^-1, b) (Denoiser.py:43-46, 80-83,
+// 163-166, 210-213).  inv_ex is linalg_solve_ex(A, I); for a row-major A torch factors the column-major view A^T
+// (LAPACK sgetrf) and solves with trans = 'T' (sgetrs).  The arithmetic below restates what MKL (2024.2, AVX-512
+// path, the library the golden fixtures were generated with) does for n = 3, operation for operation -- bit-identical
+// to torch.linalg.inv_ex on 400k random and SPD-like matrices (tests/test_capi.py::test_host_inv3_matches_torch):
+//   getrf(M = A^T): pivot = first max |m_r0|; l_r0 = m_r0 * (1 / m_00) (reciprocal, then multiply); trailing updates
+//                   fused (fma); second column: pivot, l_21 = m_21 / m_11 (a division); m_22 = fma(-l_21, m_12, m_22)
+//   info != 0 iff some U_ii is exactly zero (the reference's `mask_inversable`)
+//   U^T Y = I  forward, unfused, each row times the reciprocal of its diagonal
+//   L^T Z = Y  Z1 = fma(-l21, Z2, Y1); Z0 = Y0 - fma(l10, Z1, l20 * Z2)
+//   X = P^T Z  (rows back through the interchanges)
+// The product A^-1 b is then (a_0 b_0 + a_1 b_1) + a_2 b_2 per row, unfused, as torch's small-bmm loop sums.
+PCD_DEV bool inv3_ref(const float A[3][3], float X[3][3]) {
+    // M = A^T, rows r of M: (A[0][r], A[1][r], A[2][r]); perm tracks the original row of each pivoted row
+    float m00 = A[0][0], m01 = A[1][0], m02 = A[2][0];
+    float m10 = A[0][1], m11 = A[1][1], m12 = A[2][1];
+    float m20 = A[0][2], m21 = A[1][2], m22 = A[2][2];
+    int p0 = 0, p1 = 1, p2 = 2;
+    auto swp = [](float& a, float& b) { const float t = a; a = b; b = t; };
+    auto swpi = [](int& a, int& b) { const int t = a; a = b; b = t; };
+    // column 0: first max |m_r0|
+    {
+        const float a0 = fabsf(m00), a1 = fabsf(m10), a2 = fabsf(m20);
+        int piv = 0;
+        float best = a0;
+        if (a1 > best) { best = a1; piv = 1; }
+        if (a2 > best) { piv = 2; }
+        if (piv == 1) { swp(m00, m10); swp(m01, m11); swp(m02, m12); swpi(p0, p1); }
+        if (piv == 2) { swp(m00, m20); swp(m01, m21); swp(m02, m22); swpi(p0, p2); }
     }
-    const float x2 = b[2] / A[2][2];
-    const float x1 = (b[1] - A[1][2] * x2) / A[1][1];
-    const float x0 = (b[0] - A[0][1] * x1 - A[0][2] * x2) / A[0][0];
-    x = v3(x0, x1, x2);
+    bool ok = m00 != 0.f;
+    float l10 = m10, l20 = m20;
+    if (ok) {
+        const float r0 = 1.f / m00;
+        l10 = m10 * r0;
+        l20 = m20 * r0;
+    }
+    m11 = __builtin_fmaf(-l10, m01, m11);
+    m12 = __builtin_fmaf(-l10, m02, m12);
+    m21 = __builtin_fmaf(-l20, m01, m21);
+    m22 = __builtin_fmaf(-l20, m02, m22);
+    // column 1
+    if (fabsf(m21) > fabsf(m11)) { swp(l10, l20); swp(m11, m21); swp(m12, m22); swpi(p1, p2); }
+    ok = ok && m11 != 0.f;
+    float l21 = m21;
+    if (m11 != 0.f) l21 = m21 / m11;
+    m22 = __builtin_fmaf(-l21, m12, m22);
+    ok = ok && m22 != 0.f;
+    if (!ok) return false;
+    // U = [[m00, m01, m02], [0, m11, m12], [0, 0, m22]]; solve U^T Y = e_j, then L^T Z = Y, column by column
+    const float r00 = 1.f / m00, r11 = 1.f / m11, r22 = 1.f / m22;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const float e0 = j == 0 ? 1.f : 0.f, e1 = j == 1 ? 1.f : 0.f, e2 = j == 2 ? 1.f : 0.f;
+        const float y0 = e0 * r00;
+        const float y1 = (e1 - m01 * y0) * r11;
+        const float y2 = ((e2 - m02 * y0) - m12 * y1) * r22;
+        const float z2 = y2;
+        const float z1 = __builtin_fmaf(-l21, z2, y1);
+        const float z0 = y0 - __builtin_fmaf(l10, z1, l20 * z2);
+        // X[p_k][j] = z_k (static selects: no dynamic register index)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) X[r][j] = r == p0 ? z0 : r == p1 ? z1 : z2;
+    }
+    return true;
+}
+PCD_DEV Vec3 matvec3(const float X[3][3], Vec3 b) {
+    return v3((X[0][0] * b.x + X[0][1] * b.y) + X[0][2] * b.z, (X[1][0] * b.x + X[1][1] * b.y) + X[1][2] * b.z,
+              (X[2][0] * b.x + X[2][1] * b.y) + X[2][2] * b.z);
+}
+// x = A^-1 b as the reference computes it; false iff inv_ex reports info != 0 (the caller keeps v_i).
+PCD_DEV bool solve3(const float A[3][3], Vec3 b, Vec3& x) {
+    float X[3][3];
+    if (!inv3_ref(A, X)) return false;
+    x = matvec3(X, b);
     return true;
 }
 

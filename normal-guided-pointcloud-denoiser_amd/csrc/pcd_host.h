@@ -25,6 +25,40 @@ int fail(int code, const std::string& msg);
 #define PCD_LAUNCH_CHECK() PCD_HIP(hipGetLastError())
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Stream-ordered temporaries of one entry point: every pointer taken through alloc() is released with hipFreeAsync
+// on every exit path (an early PCD_HIP / PCD_CHECK_ARG return included), and the destructor then synchronises the
+// stream so no caller sees a call return with its scratch still in use.
+struct StreamTemps {
+    hipStream_t st;
+    void* p[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    int n = 0;
+    explicit StreamTemps(hipStream_t s) : st(s) {}
+    template <class T>
+    hipError_t alloc(T** out, size_t bytes) {
+        *out = nullptr;
+        if (n == 8) return hipErrorInvalidValue;
+        void* q = nullptr;
+        const hipError_t e = hipMallocAsync(&q, bytes, st);
+        if (e == hipSuccess) { p[n++] = q; *out = static_cast<T*>(q); }
+        return e;
+    }
+    // free everything now (stream-ordered; sync: and wait for the stream), reporting the first failure
+    hipError_t release(bool sync = true) {
+        hipError_t first = hipSuccess;
+        for (int i = 0; i < n; ++i) {
+            const hipError_t e = hipFreeAsync(p[i], st);
+            if (first == hipSuccess) first = e;
+            p[i] = nullptr;
+        }
+        n = 0;
+        const hipError_t e = sync ? hipStreamSynchronize(st) : hipSuccess;
+        return first == hipSuccess ? e : first;
+    }
+    ~StreamTemps() { if (n) (void)release(); }
+    StreamTemps(const StreamTemps&) = delete;
+    StreamTemps& operator=(const StreamTemps&) = delete;
+};
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // One 16-byte hash slot: Morton key of an occupied cell -> [start, end) in the sorted snapshot.

@@ -324,7 +324,9 @@ PCD_DEV Vec3 step_feature(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float
         }
     const Vec3 b = ((vi + outer_mul(ni, vi)) + outer_mul(ni, svj)) + snv;
     Vec3 x;
-    if (!solve3(A, b, x)) x = vi;
+    // optimal_pos[mask] = optimal_pos[mask] + (new_pos[mask] - optimal_pos[mask])  (Denoiser.py:167, 214)
+    if (solve3(A, b, x)) x = vi + (x - vi);
+    else x = vi;
     return clamp_step(vi, x, alpha, d);
 }
 

@@ -17,7 +17,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PCD_LIB", os.path.join(os.path.dirname(_HERE), "libpcd.so"))
 
 PCD_OK, PCD_ERR_ARG, PCD_ERR_OOM, PCD_ERR_HIP, PCD_ERR_STATE, PCD_ERR_RCCL = 0, -1, -2, -3, -4, -5
-FIELD_POS, FIELD_NRM, FIELD_FN = 0, 1, 2
+DT_F32, DT_F64, DT_I32 = 0, 1, 2
+OP_SUM, OP_MAX = 0, 1
+FIELD_POS, FIELD_NRM, FIELD_FN, FIELD_EDGE = 0, 1, 2, 3
 (STAGE_KNN_NVT1, STAGE_NVT2, STAGE_PHASE_SUM, STAGE_PHASE_CENTRE, STAGE_PHASE_MAXDIST, STAGE_PHASE_APPLY,
  STAGE_FINISH) = range(7)
 STEP_FLAT, STEP_EDGE, STEP_FEATURE, STEP_CORNER, STEP_NEW, STEP_DUMMY = range(6)
@@ -30,6 +32,12 @@ class PcdError(RuntimeError):
 class _GridInfo(ctypes.Structure):
     _fields_ = [("n", c_int64), ("cells", c_int64), ("table_slots", c_int64), ("cell", c_float),
                 ("origin", c_float * 3), ("dims", ctypes.c_int32 * 3)]
+
+
+class CpsdParams(ctypes.Structure):
+    """Mirror of ``pcd_cpsd_params`` (include/pcd.h)."""
+    _fields_ = [("r", c_float), ("rho", c_float), ("tau", c_float), ("damp", c_float), ("d", c_float),
+                ("step_clamp", c_float), ("alpha", c_float * 3), ("k_update", c_int)]
 
 
 class DenoiseParams(ctypes.Structure):
@@ -96,11 +104,23 @@ _SIGS = {
     "pcd_denoiser_pack": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "pcd_denoiser_unpack": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "pcd_denoiser_get_timing": (c_int, [c_void_p, POINTER(c_float), c_int, POINTER(c_int)]),
+    "pcd_cpsd_iterate": (c_int, [c_void_p, POINTER(CpsdParams), c_int, c_void_p]),
+    "pcd_comm_id_bytes": (c_int, []),
+    "pcd_comm_id": (c_int, [c_void_p]),
+    "pcd_comm_create": (c_int, [c_void_p, c_int, c_int, POINTER(c_void_p)]),
+    "pcd_comm_create_host": (c_int, [c_void_p, c_int, c_int, POINTER(c_void_p)]),
+    "pcd_comm_destroy": (c_int, [c_void_p]),
+    "pcd_allreduce_scalars": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "pcd_denoiser_set_routes": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p]),
+    "pcd_halo_exchange": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "pcd_slab_iterate": (c_int, [c_void_p, c_void_p, POINTER(DenoiseParams), c_int, c_void_p]),
     "pcd_orient_normals_mst": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64]),
     "pcd_orient_normals_mst_gpu": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p]),
     "pcd_host_eigh3": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "pcd_host_vu_smooth": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p]),
     "pcd_host_solve3": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "pcd_host_inv3": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "pcd_host_nvt_tensor": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p]),
 }
 
@@ -393,6 +413,36 @@ class FusedDenoiser:
         check(lib().pcd_denoiser_unpack(self.handle, int(field), ptr(rows), rows.numel(), ptr(data),
                                         c_void_p(stream_ptr())), "pcd_denoiser_unpack")
 
+    # ---- spatial slabs in one call per iteration (pcd_denoiser_set_routes / pcd_slab_iterate, include/pcd.h)
+    def set_routes(self, peers, send_rows, recv_rows, own_lo=None, own_hi=None):
+        """peers: list of peer ranks; send_rows / recv_rows: per peer an integer tensor of spatial-order rows.  The
+        library copies them.  own_lo / own_hi: the owned slab's box (enables the exchange / compute overlap)."""
+        npeers = len(peers)
+        pa = (c_int * max(npeers, 1))(*[int(q) for q in peers])
+        ns = (c_int64 * max(npeers, 1))(*[int(r.numel()) for r in send_rows])
+        nr = (c_int64 * max(npeers, 1))(*[int(r.numel()) for r in recv_rows])
+        dev = device()
+        cat = lambda rs: (torch.cat([self._rows_i32(r) for r in rs]) if rs and sum(r.numel() for r in rs)
+                          else torch.zeros(1, dtype=torch.int32, device=dev))
+        sr, rr = cat(send_rows), cat(recv_rows)
+        lo3 = None if own_lo is None else (c_float * 3)(*[float(v) for v in own_lo])
+        hi3 = None if own_hi is None else (c_float * 3)(*[float(v) for v in own_hi])
+        check(lib().pcd_denoiser_set_routes(self.handle, npeers, pa, ns, ptr(sr), nr, ptr(rr), lo3, hi3,
+                                            c_void_p(stream_ptr())), "pcd_denoiser_set_routes")
+
+    def cpsd_iterate(self, params: "CpsdParams", iterations: int):
+        """The CPSD driver's iterations on the loaded state (pcd_cpsd_iterate)."""
+        check(lib().pcd_cpsd_iterate(self.handle, ctypes.byref(params), int(iterations), c_void_p(stream_ptr())),
+              "pcd_cpsd_iterate")
+
+    def slab_iterate(self, comm: "Comm", params: DenoiseParams, iterations: int = 1):
+        check(lib().pcd_slab_iterate(self.handle, comm.handle, ctypes.byref(params), int(iterations),
+                                     c_void_p(stream_ptr())), "pcd_slab_iterate")
+
+    def halo_exchange(self, comm: "Comm", field: int):
+        check(lib().pcd_halo_exchange(self.handle, comm.handle, int(field), c_void_p(stream_ptr())),
+              "pcd_halo_exchange")
+
     TIMING_SLOTS = ("anchor_test", "requery", "spill_search", "nvt1", "nvt2", "flat_phase", "edge_phase",
                     "corner_phase", "finish")
 
@@ -402,6 +452,101 @@ class FusedDenoiser:
         nw = c_int(0)
         check(lib().pcd_denoiser_get_timing(self.handle, buf, 16, ctypes.byref(nw)), "pcd_denoiser_get_timing")
         return [buf[i] for i in range(nw.value)]
+
+
+# ----------------------------------------------------------------------------------------------- slab transport
+_EXCHANGE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int, POINTER(c_int), POINTER(c_float), POINTER(c_int64),
+                                POINTER(c_float), POINTER(c_int64))
+_ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_int, c_int, c_int)
+
+
+class _HostTransport(ctypes.Structure):
+    _fields_ = [("user", c_void_p), ("exchange", _EXCHANGE_FN), ("allreduce", _ALLREDUCE_FN)]
+
+
+class Comm:
+    """The slab transport of libpcd (pcd_comm): RCCL, or host callbacks over a torch.distributed CPU group (gloo)."""
+
+    def __init__(self, handle, keep=None):
+        self.handle = handle
+        self._keep = keep
+
+    @staticmethod
+    def rccl(world: int, rank: int, broadcast) -> "Comm":
+        """Collective: rank 0 makes an RCCL unique id, `broadcast(uint8 tensor)` (in place, from rank 0) hands it to
+        every rank, and every rank joins the communicator on its current HIP device."""
+        L = lib()
+        nb = L.pcd_comm_id_bytes()
+        buf = (ctypes.c_ubyte * nb)()
+        if rank == 0:
+            check(L.pcd_comm_id(buf), "pcd_comm_id")
+        t = torch.tensor(bytearray(buf), dtype=torch.uint8)
+        t = broadcast(t)
+        ctypes.memmove(buf, bytes(t.cpu().numpy().tobytes()), nb)
+        h = c_void_p()
+        check(L.pcd_comm_create(buf, int(world), int(rank), ctypes.byref(h)), "pcd_comm_create")
+        return Comm(h)
+
+    @staticmethod
+    def host(world: int, rank: int, exchange, allreduce) -> "Comm":
+        """exchange(peers, send [ns, 4] f32 array, send_off, recv [nr, 4] array to fill, recv_off) and
+        allreduce(buf array, op) over numpy views of the library's host staging buffers (no copies)."""
+        import numpy as np
+
+        def _ex(user, npeers, peers, send, soff, recv, roff):
+            try:
+                P = [peers[q] for q in range(npeers)]
+                so = [soff[q] for q in range(npeers + 1)]
+                ro = [roff[q] for q in range(npeers + 1)]
+                sa = np.ctypeslib.as_array(send, shape=(max(so[-1], 1) * 4,)).reshape(-1, 4)
+                ra = np.ctypeslib.as_array(recv, shape=(max(ro[-1], 1) * 4,)).reshape(-1, 4)
+                exchange(P, sa, so, ra, ro)
+                return 0
+            except Exception as e:                              # noqa: BLE001  (reported as a status code)
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        def _ar(user, buf, count, dtype, op):
+            try:
+                dt = {DT_F32: np.float32, DT_F64: np.float64, DT_I32: np.int32}[dtype]
+                arr = np.frombuffer((ctypes.c_char * (count * np.dtype(dt).itemsize)).from_address(buf), dtype=dt)
+                allreduce(arr, op)
+                return 0
+            except Exception:                                   # noqa: BLE001
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        cbs = _HostTransport(None, _EXCHANGE_FN(_ex), _ALLREDUCE_FN(_ar))
+        h = c_void_p()
+        check(lib().pcd_comm_create_host(ctypes.byref(cbs), int(world), int(rank), ctypes.byref(h)),
+              "pcd_comm_create_host")
+        return Comm(h, keep=(cbs, _ex, _ar))
+
+    def allreduce_(self, t: torch.Tensor, op: int = OP_SUM) -> torch.Tensor:
+        """In-place all-reduce of a small device tensor (float32 / float64 / int32)."""
+        dt = {torch.float32: DT_F32, torch.float64: DT_F64, torch.int32: DT_I32}[t.dtype]
+        assert t.is_contiguous() and t.is_cuda
+        check(lib().pcd_allreduce_scalars(self.handle, ptr(t), t.numel(), dt, int(op), c_void_p(stream_ptr())),
+              "pcd_allreduce_scalars")
+        return t
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.pcd_comm_destroy(h)
+            self.handle = None
+
+
+def make_cpsd_params(r, d, rho=0.9, tau=0.3, damp=3.0, step_clamp=None, alphas=(0.1, 1.0, 1.0), k_update=8):
+    p = CpsdParams()
+    p.r, p.rho, p.tau, p.damp, p.d = float(r), float(rho), float(tau), float(damp), float(d)
+    p.step_clamp = float(d * 20000.0 if step_clamp is None else step_clamp)
+    for a in range(3):
+        p.alpha[a] = float(alphas[a])
+    p.k_update = int(k_update)
+    return p
 
 
 def make_params(k=16, k_update=8, rho=None, tau=0.3, damp=3.0, class_scale=0.2, d=1.0,
@@ -588,6 +733,16 @@ def host_solve3(a, b):
     ok = np.zeros(b.shape[0], np.int32)
     check(lib().pcd_host_solve3(a.ctypes.data, b.ctypes.data, b.shape[0], x.ctypes.data, ok.ctypes.data),
           "pcd_host_solve3")
+    return x, ok.astype(bool)
+
+
+def host_inv3(a):
+    """torch.linalg.inv_ex's arithmetic for 3x3 as the position steps restate it (host build): (inverse, ok)."""
+    import numpy as np
+    a = np.ascontiguousarray(a, np.float32)
+    x = np.zeros_like(a)
+    ok = np.zeros(a.shape[0], np.int32)
+    check(lib().pcd_host_inv3(a.ctypes.data, a.shape[0], x.ctypes.data, ok.ctypes.data), "pcd_host_inv3")
     return x, ok.astype(bool)
 
 

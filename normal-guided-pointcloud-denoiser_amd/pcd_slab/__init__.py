@@ -5,8 +5,12 @@ of slab r and holds, in addition, a HALO: every snapshot point whose coordinate 
 of the slab.  Its grid is built over owned + halo points on the global cell lattice (pcd_grid_params), so its
 spatial order is a subsequence of the one-GPU order and distance ties break exactly as on one GPU.
 
-Per iteration the rank runs the fused loop's stages on its OWN rows only (pcd_denoiser_stage) and keeps the halo
-rows current between stages (the only places a stage reads another rank's points):
+Per iteration the rank runs the fused loop on its OWN rows only and keeps the halo rows current between stages (the
+only places a stage reads another rank's points).  The product path is ONE library call per iteration
+(pcd_slab_iterate: the stages, the RCCL halo exchanges on a stream of their own, overlapped with the rows that read
+no halo row, and the two all-reduces; libpcd owns the RCCL communicator, pcd_comm).  The same sequence also runs
+stage by stage from Python (native=False: pcd_denoiser_stage + pack/unpack + torch.distributed), the path the CPU
+tests drive with an oracle engine:
     KNN_NVT1                        kNN + first vote + VU smoothing of own points
     exchange FN                     NVT2 reads the smoothed normals of the neighbours
     NVT2                            classes + edge vectors
@@ -132,6 +136,31 @@ class TorchTransport:
                 req.wait()
         return {p: (b.to(device) if self.host else b) for p, b in outs.items()}
 
+    def native_comm(self) -> "nat.Comm":
+        """libpcd's transport for pcd_slab_iterate (collective): an RCCL communicator of its own when this group is
+        NCCL (= RCCL), else host callbacks over this (gloo) group -- the same library code path, each exchange staged
+        through pinned host memory."""
+        dist, grp = self.dist, self.group
+        if not self.host:
+            return nat.Comm.rccl(self.world, self.rank, lambda t: self.broadcast_(t.to(nat.device()), 0).cpu())
+
+        def exchange(peers, send, soff, recv, roff):
+            ops = []
+            for q, peer in enumerate(peers):
+                if roff[q + 1] > roff[q]:
+                    ops.append(dist.P2POp(dist.irecv, torch.from_numpy(recv[roff[q]:roff[q + 1]]), peer, grp))
+                if soff[q + 1] > soff[q]:
+                    ops.append(dist.P2POp(dist.isend, torch.from_numpy(send[soff[q]:soff[q + 1]].copy()), peer, grp))
+            if ops:
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+
+        def allreduce(buf, op):
+            t = torch.from_numpy(buf)
+            dist.all_reduce(t, dist.ReduceOp.MAX if op == nat.OP_MAX else dist.ReduceOp.SUM, grp)
+
+        return nat.Comm.host(self.world, self.rank, exchange, allreduce)
+
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.host and t.device.type != "cpu":
             h = t.cpu()
@@ -167,6 +196,11 @@ class LocalTransport:
     def broadcast_(self, t, src=0):
         return t
 
+    def native_comm(self):
+        def never(*_):
+            raise RuntimeError("world 1 has nothing to exchange")
+        return nat.Comm.host(1, 0, never, never)
+
 
 # ----------------------------------------------------------------------------------------------- HIP engine
 class HipSlabEngine:
@@ -184,7 +218,8 @@ class HipSlabEngine:
         self.fused.load(local_pos.to(dev), local_n.to(dev))
         self.fused.set_seeding(seeding)
         own_rows = torch.sort(self.row_of[owned_local.to(dev)]).values.to(torch.int32)
-        self.fused.set_rows(own_rows)
+        # every local point owned (one rank): all rows, no row list (the single-GPU launch shapes)
+        self.fused.set_rows(None if own_rows.numel() == self.n else own_rows)
         self.fused.set_coverage(*coverage)
         self.red4 = torch.zeros(4, dtype=torch.float64, device=dev)
         self.red1 = torch.zeros(1, dtype=torch.float32, device=dev)
@@ -206,6 +241,27 @@ class HipSlabEngine:
 
     def status(self) -> int:
         return self.fused.status()
+
+    # the one-call iteration (pcd_slab_iterate)
+    native = True
+
+    def set_routes(self, peers, send_rows, recv_rows, own_lo, own_hi):
+        self.fused.set_routes(peers, send_rows, recv_rows, own_lo, own_hi)
+
+    def slab_iterate(self, comm, params, iterations=1):
+        self.fused.slab_iterate(comm, params, iterations)
+
+    def slab_iterate_timed(self, comm, params) -> dict:
+        """One slab iteration with the library's per-stage HIP events (pcd_denoiser_set_timing), ms."""
+        self.fused.set_timing(True)
+        self.fused.slab_iterate(comm, params, 1)
+        slots = self.fused.timing()
+        self.fused.set_timing(False)
+        names = nat.FusedDenoiser.TIMING_SLOTS
+        out = {names[i]: float(slots[i]) for i in range(min(len(slots), len(names)))}
+        out["knn_nvt1"] = float(sum(slots[:4]))
+        out["iteration"] = float(sum(slots))
+        return out
 
     def set_state(self, local_idx, pos, n):
         """Current positions / normals of the given local points (a re-planned rank taking over the state)."""
@@ -239,7 +295,9 @@ class SlabDenoiser:
     recovery."""
 
     def __init__(self, snap_pos, snap_n, k_max, transport=None, halo=None, engine_factory=None, seeding=True,
-                 k_hint=None, check_every=1, halo_growth=2.0, max_replans=4, weights=None):
+                 k_hint=None, check_every=1, halo_growth=2.0, max_replans=4, weights=None, native=None):
+        """native: one pcd_slab_iterate call per iteration over libpcd's own transport (default for the HIP engine);
+        False: the same stages driven from Python over torch.distributed."""
         self.t = transport or LocalTransport()
         rank, world = self.t.rank, self.t.world
         if world > 1:
@@ -256,6 +314,8 @@ class SlabDenoiser:
         # cell lattice of the ranks' snapshot indices: the fused loop's (pcd_native.fused_k_hint) unless given
         self.k_max, self.k_hint, self.seeding = k_max, k_hint or nat.fused_k_hint(k_max) or 32, seeding
         self.engine_factory = engine_factory
+        self.native = (engine_factory is None) if native is None else bool(native)
+        self.comm = self.t.native_comm() if self.native else None
         self.check_every, self.halo_growth, self.max_replans = int(check_every), float(halo_growth), int(max_replans)
         self.replans = 0
         self.e = None
@@ -303,6 +363,22 @@ class SlabDenoiser:
             if inc.numel():
                 self.recv_rows[peer] = self.e.rows(to_local[inc])
         self.halo_points = sum(r.numel() for r in self.recv_rows.values())
+        if self.native:
+            # routes + the OWNED slab (the rows whose k-ball stays strictly inside it read no halo row: NVT2 / the
+            # phases run them while an exchange is in flight).  Strict bounds: a snapshot point ON a cut may be owned
+            # by the neighbour, so the box is shrunk by one float32 ulp on the cut faces.
+            import numpy as np
+            big = 3.0e38
+            lo, hi = [-big] * 3, [big] * 3
+            if rank > 0:
+                lo[plan.axis] = float(np.nextafter(np.float32(plan.lo[rank]), np.float32(np.inf)))
+            if rank < world - 1:
+                hi[plan.axis] = float(np.nextafter(np.float32(plan.hi[rank]), np.float32(-np.inf)))
+            peers = sorted(set(self.send_rows) | set(self.recv_rows))
+            empty = torch.zeros(0, dtype=torch.int32, device=nat.device())
+            self.e.set_routes(peers, [self.send_rows.get(q, empty) for q in peers],
+                              [self.recv_rows.get(q, empty) for q in peers], lo if peers else None,
+                              hi if peers else None)
 
     def _owned_state_now(self):
         """(pos, n) of this rank's own points, owned-local order (a checkpoint)."""
@@ -394,6 +470,9 @@ class SlabDenoiser:
 
     def _one(self, params):
         e = self.e
+        if self.native:
+            e.slab_iterate(self.comm, params, 1)
+            return
         e.stage(params, nat.STAGE_KNN_NVT1)
         self._exchange(nat.FIELD_FN)
         e.stage(params, nat.STAGE_NVT2)
@@ -417,7 +496,11 @@ class SlabDenoiser:
 
     def rebalance(self, class_weights=(1.0, 1.3, 1.4)):
         """Re-cut the slabs by cost: each point weighs class_weights[its class in the last NVT2 stage] (flat, edge,
-        corner: the edge / feature steps solve a 3x3 system over their neighbours).  Collective."""
+        corner: the edge / feature steps solve a 3x3 system over their neighbours).  Collective.  Iterations since the
+        last coverage check are verified first (a thin halo there re-plans and replays them), so the state carried
+        into the new cut is exact."""
+        if self.check_every > 0 and self._since > 0:
+            self._verify()
         cls = self.e.classes()
         cls = cls[self.owned_local.to(cls.device)]
         w_tab = torch.tensor(class_weights, dtype=torch.float32, device=cls.device)
@@ -428,6 +511,8 @@ class SlabDenoiser:
 
     def iterate_timed(self, params) -> dict:
         """One iteration with CUDA/HIP events on the launch stream around each stage group (ms)."""
+        if self.native:
+            return self.e.slab_iterate_timed(self.comm, params)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
         e = self.e
         ev[0].record()

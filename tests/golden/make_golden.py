@@ -22,6 +22,9 @@ Every fixture records which reference entry point produced it:
                     pos / errors / iteration count and the error trajectory
   thesis.npz        the thesis driver "Ours" (PostProcessing.ipynb:1069-1090) on fandisk: 2 iterations, Jacobi
                     across classes, flat_step + feature_step at d*20000, global clamp ||temp_pos - original_pos|| < d
+  cpsd.npz          the CPSD ("Martin") path: radius selections, normal-filtered NVT / PVT, VU features, corner_step,
+                    getVUDecomposition, and 2 iterations of the notebook's 50-iteration driver (PostProcessing.ipynb
+                    :1041-1062, j == 1) verbatim: positions, normals, classes and clamp mask per iteration
   io.npz            Object.Pointcloud.loadObj readback of models/fandisk.obj (Object.py:71-89)
 """
 from __future__ import annotations
@@ -345,6 +348,40 @@ def gen_cpsd(out_dir):
     vu = proc.getVUDecomposition()
     res["vud_eigval"] = np32(vu.eigval)
     res["vud_eigvec"] = np32(vu.eigvec)
+    # the CPSD driver itself: PostProcessing.ipynb:1041-1062 (j == 1, "Martin") verbatim for 2 of its 50
+    # iterations on fandisk -- radius decomposition, VU classes, flat / edge / corner steps at d*20000 (Jacobi across
+    # classes through temp_pos), the global clamp ||temp_pos - original_pos|| < d, n := f_n
+    col_value = Processor(Pointcloud(pos0.clone(), n0.clone()))
+    l = TorchUtils.averageEdgeLength(col_value.graph.pos, col_value.selector.getKNNSelection(6).getEdgeIndex())
+    dd = 2 * l
+    original_pos = col_value.graph.pos.clone()
+    res["drv_d"] = np.float64(dd)
+    alphas = [0.1, 1, 1]
+    for it in range(2):
+        decomposition, f_n = col_value.getMartinFeatureDecomposition(r=dd)
+        classes = decomposition.getVUFeatures(tau=0.3)
+        selection = col_value.selector.getKNNSelection(k=8)
+        temp_pos = col_value.graph.pos.clone()
+        for key in range(3):
+            indices = (classes == key).nonzero().flatten()
+            if indices.size(0) == 0:
+                continue
+            elif key == 0:
+                new_pos = col_value.denoiser.flat_step(selection.filter(indices), f_n, dd * 20000, alphas[key])
+            elif key == 1:
+                edge_vectors = decomposition.eigvec[..., 0]
+                new_pos = col_value.denoiser.edge_step(selection.filter(indices), f_n, edge_vectors, dd * 20000,
+                                                       alphas[key])
+            else:
+                new_pos = col_value.denoiser.corner_step(selection.filter(indices), f_n, dd * 20000, alphas[key])
+            temp_pos[indices] = new_pos
+        mask = (temp_pos - original_pos).norm(dim=1) < dd
+        col_value.graph.pos[mask] = temp_pos[mask]
+        col_value.graph.n = f_n
+        res[f"drv_pos_it{it + 1}"] = np32(col_value.graph.pos)
+        res[f"drv_n_it{it + 1}"] = np32(col_value.graph.n)
+        res[f"drv_classes_it{it + 1}"] = classes.numpy().astype(np.int64)
+        res[f"drv_mask_it{it + 1}"] = mask.numpy()
     np.savez_compressed(os.path.join(out_dir, "cpsd.npz"), **res)
     lens = np.diff(res["sel_r1_slices"])
     print(f"cpsd: r={d:.5f} neighbours/pt {lens.mean():.1f} (min {lens.min()}, max {lens.max()}), "

@@ -139,24 +139,26 @@ def test_cpsd_corner_step(cpsd, proc):
     assert np.median(dev) < 1e-6 and np.percentile(dev, 99) < 1e-4, np.percentile(dev, [50, 99, 100])
 
 
-def test_cpsd_driver_matches_oracle(cpsd, gpu):
+def test_cpsd_driver_matches_reference(cpsd, gpu):
     """The 50-iteration CPSD driver (PostProcessing.ipynb:1041-1062) as Processor.cpsdDenoise: its first two
-    iterations against the oracle's composition of the same operators (pcd_oracle.cpsd_iteration) on the fandisk
-    fixture -- one iteration at the single-iteration tolerances of test_gpu_parity (median 1e-6, p99 3e-4 x bbox),
-    the second within the loop's chaotic envelope; the global clamp holds."""
+    iterations against the REFERENCE's own run of the notebook loop on fandisk (make_golden.py gen_cpsd: drv_pos_it1/2,
+    d = 2 l as the notebook computes it) -- one iteration at the single-iteration tolerances of test_gpu_parity (median
+    1e-6, p99 3e-4 x bbox), the second within the loop's chaotic envelope; the global clamp holds."""
     pos0, n0 = cpsd["pos"], cpsd["n"]
-    d = float(cpsd["d"])
+    d = float(cpsd["drv_d"])
     bbox = float(np.linalg.norm(pos0.max(0) - pos0.min(0)))
-    knn = O.FrozenKNN(pos0)
-    rp, rn = pos0.copy(), n0.copy()
     for it in (1, 2):
-        rp, rn = O.cpsd_iteration(pos0, rp, rn, pos0, knn, d)
+        ref = cpsd[f"drv_pos_it{it}"]
         v = T(pos0, gpu).clone()
         proc = Processor(Pointcloud(v, T(n0, gpu).clone()))
         proc.cpsdDenoise(iterations=it, d=d)                         # original_pos = the call's input, as the ipynb
-        dev = np.linalg.norm(v.cpu().numpy() - rp, axis=1) / bbox
+        dev = np.linalg.norm(v.cpu().numpy() - ref, axis=1) / bbox
+        print(f"cpsd driver it{it}: exact {np.mean(dev == 0):.4f} median {np.median(dev):.3g} "
+              f"p99 {np.percentile(dev, 99):.3g} max {dev.max():.3g}")
         if it == 1:
             assert np.median(dev) < 1e-6 and np.percentile(dev, 99) < 3e-4, (np.median(dev), np.percentile(dev, 99))
+            nd = np.abs(proc.graph.n.cpu().numpy() - cpsd["drv_n_it1"]).max(1)
+            assert np.percentile(nd, 99) < 1e-5, np.percentile(nd, 99)
         else:
             assert np.median(dev) < 1e-5 and np.percentile(dev, 99) < 5e-3, (np.median(dev), np.percentile(dev, 99))
         assert proc.graph.pos is v                                   # updated in place

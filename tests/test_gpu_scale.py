@@ -84,6 +84,15 @@ def test_headline_10m_25_iterations_bitwise(gpu):
     assert redo[0] == 10_000_000 and min(redo[1:]) > 10_000, redo
 
 
+def test_headline_workload_2m_40_iterations_bitwise(gpu):
+    """Past the re-anchoring peak (iterations 25-40 re-anchor ~9 % of the rows a step): 2M points of the
+    headline workload for 40 anchored iterations, state bitwise against the reset-seed path after every one."""
+    pos, nrm = bunny_cloud(2_000_000, 2, 0.005)
+    redo, _ = run_pair(pos, nrm, 32, 40, gpu)
+    assert redo[0] == 2_000_000 and min(redo[1:]) > 0, redo
+    assert max(redo[20:]) > 0.02 * 2_000_000, redo        # the peak window really re-anchors at scale
+
+
 def test_config5_80m_one_gpu_bitwise(gpu):
     """BASELINE configs[4]'s whole 80M-point cloud (the bench's slab workload: bench.make_cloud seed 3, sampled on
     the device) on ONE MI355X: 3 anchored iterations against the reset-seed path (every kNN an unseeded grid

@@ -34,11 +34,11 @@ def _params(d, jacobi=False):
     return nat.make_params(k=K, k_update=KU, d=d * 20000, phases=ph, jacobi=True, clamp_global=d)
 
 
-def _fused(pos, nrm, d, jacobi=False):
+def _fused(pos, nrm, d, jacobi=False, iters=ITERS):
     g = nat.Grid(pos, k_hint=K)
     fd = nat.FusedDenoiser(g, max(K, KU))
     fd.load(pos, nrm)
-    fd.iterate(_params(d, jacobi), ITERS)
+    fd.iterate(_params(d, jacobi), iters)
     p, n = torch.empty_like(pos), torch.empty_like(nrm)
     fd.store(p, n)
     return p.cpu().numpy(), n.cpu().numpy()
@@ -63,7 +63,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=False):
+def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=False, native=None):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -77,7 +77,7 @@ def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=F
         c = np.load(cloud_path)
         pos, nrm = torch.from_numpy(c["pos"]).to(dev), torch.from_numpy(c["n"]).to(dev)
         tr = TorchTransport()
-        sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K)
+        sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K, native=native)
         sd.iterate(_params(d, jacobi), ITERS)
         sd.check()
         p, n = gather_global(sd.owned_state(), pos.size(0), tr)
@@ -105,6 +105,42 @@ def test_hip_slab_world2_matches_one_gpu(gpu, tmp_path):
 
 
 @pytest.mark.gpu
+def test_hip_slab_world1_staged_is_the_fused_loop(gpu):
+    """The Python-driven stage sequence (native=False: pcd_denoiser_stage + pack/unpack), the reference the one-call
+    path is checked against, is itself the fused loop bit for bit."""
+    pos, nrm = _cloud(gpu)
+    d = _d(pos)
+    sd = SlabDenoiser(pos, nrm, max(K, KU), transport=LocalTransport(), k_hint=K, native=False)
+    sd.iterate(nat.make_params(k=K, k_update=KU, d=d), ITERS)
+    sd.check()
+    p, n = gather_global(sd.owned_state(), pos.size(0), sd.t)
+    rp, rn = _fused(pos, nrm, d)
+    np.testing.assert_array_equal(p.cpu().numpy(), rp)
+    np.testing.assert_array_equal(n.cpu().numpy(), rn)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jacobi", [False, True], ids=["gauss_seidel", "jacobi"])
+def test_hip_slab_world2_one_call_equals_staged(gpu, tmp_path, jacobi):
+    """pcd_slab_iterate (one library call per iteration: its exchanges on a stream of their own, overlapped with the
+    rows whose k-ball stays inside the owned slab; here over the host-callback transport on gloo) against the same
+    stages driven one by one from Python: bit-identical."""
+    import torch.multiprocessing as mp
+    pos, nrm = _cloud(gpu)
+    d = _d(pos)
+    cloud = str(tmp_path / "cloud.npz")
+    np.savez(cloud, pos=pos.cpu().numpy(), n=nrm.cpu().numpy())
+    got = {}
+    for native in (True, False):
+        out = str(tmp_path / f"slab2_{native}.npz")
+        mp.spawn(_worker, args=(2, _free_port(), out, cloud, d, "gloo", jacobi, native), nprocs=2, join=True)
+        got[native] = np.load(out)
+    assert int(got[True]["halo"]) > 0
+    np.testing.assert_array_equal(got[True]["pos"], got[False]["pos"])
+    np.testing.assert_array_equal(got[True]["n"], got[False]["n"])
+
+
+@pytest.mark.gpu
 def test_hip_slab_world4_matches_one_gpu(gpu, tmp_path):
     """Four ranks sharing the GPU over gloo: two interior slabs exchange halos with a neighbour on either side,
     as the interior ranks of the 8-GPU run do."""
@@ -122,7 +158,8 @@ def test_hip_slab_world4_matches_one_gpu(gpu, tmp_path):
     np.testing.assert_allclose(res["n"], rn, rtol=0, atol=1e-5)
 
 
-def _worker_owned(rank, world, port, out_prefix, cloud_path, d, halo=None):
+def _worker_owned(rank, world, port, out_prefix, cloud_path, d, halo=None, iters=ITERS, check_every=1,
+                  rebalance_after=None):
     """Like _worker, but every rank saves its own points (ids, pos, n) -- no all-gather of the whole cloud."""
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -134,13 +171,20 @@ def _worker_owned(rank, world, port, out_prefix, cloud_path, d, halo=None):
         c = np.load(cloud_path)
         pos, nrm = torch.from_numpy(c["pos"]).to(dev), torch.from_numpy(c["n"]).to(dev)
         tr = TorchTransport()
-        sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K, halo=halo)
+        sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K, halo=halo, check_every=check_every)
         del pos, nrm
-        sd.iterate(_params(d), ITERS)
+        owned0 = sd.owned_global.numel()
+        if rebalance_after is None:
+            sd.iterate(_params(d), iters)
+        else:
+            sd.iterate(_params(d), rebalance_after)
+            sd.rebalance()
+            sd.iterate(_params(d), iters - rebalance_after)
+        sd._verify()                    # the iterations since the last check (the bench's exactness check)
         sd.check()
         ids, p, n = sd.owned_state()
         np.savez(f"{out_prefix}_{rank}.npz", ids=ids.cpu().numpy(), pos=p.cpu().numpy(), n=n.cpu().numpy(),
-                 halo=sd.halo_points, replans=sd.replans)
+                 halo=sd.halo_points, replans=sd.replans, owned=[owned0, ids.numel()])
     finally:
         dist.destroy_process_group()
 
@@ -176,6 +220,57 @@ def test_hip_slab_world8_8m_points_matches_one_gpu(gpu, tmp_path):
     dev = np.abs(p - rp).max()
     assert dev <= 1e-6 * bbox, dev / bbox
     np.testing.assert_allclose(nn, rn, rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_hip_slab_world8_rebalance_12_iterations_matches_one_gpu(gpu, tmp_path):
+    """What the bench's slab mode runs: 8 ranks (sharing the box's GPU over gloo) on 8M points, cut re-balanced by
+    class cost after the second iteration (rebalance() on the HIP engine), coverage checked every 10 iterations
+    (check_every=10: one checkpoint / verify cycle inside the run, the second at the end), 12 one-call iterations --
+    against the one-GPU fused loop within 1e-6 x bbox."""
+    import torch.multiprocessing as mp
+    n, iters = 8_000_000, 12
+    pos, nrm = _cloud(gpu, n=n, seed=3)
+    d = _d(pos)
+    prefix, cloud = str(tmp_path / "reb8"), str(tmp_path / "cloud.npz")
+    np.savez(cloud, pos=pos.cpu().numpy(), n=nrm.cpu().numpy())
+    mp.spawn(_worker_owned, args=(8, _free_port(), prefix, cloud, d, None, iters, 10, 2), nprocs=8, join=True)
+    p, nn, halos, replans = _assemble(prefix, 8, n)
+    owned = np.stack([np.load(f"{prefix}_{r}.npz")["owned"] for r in range(8)])
+    assert not np.isnan(p).any() and min(halos) > 0
+    assert (owned[:, 0] != owned[:, 1]).any() and owned[:, 1].sum() == n      # the cut moved; every point owned
+    rp, rn = _fused(pos, nrm, d, iters=iters)
+    bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
+    dev = np.abs(p - rp).max()
+    assert dev <= 1e-6 * bbox, dev / bbox
+    np.testing.assert_allclose(nn, rn, rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_rccl_comm_world1_exchange_and_allreduce(gpu):
+    """libpcd's own RCCL communicator (pcd_comm_create from pcd_comm_id) on one GPU: a halo route to itself moves
+    rows through ncclSend / ncclRecv (pack -> RCCL -> unpack on the library's exchange stream), and the in-place
+    scalar all-reduces run through ncclAllReduce."""
+    pos, nrm = _cloud(gpu, 5000)
+    g = nat.Grid(pos, k_hint=K)
+    fd = nat.FusedDenoiser(g, K)
+    fd.load(pos, nrm)
+    comm = nat.Comm.rccl(1, 0, lambda t: t)
+    rows = torch.arange(pos.size(0), dtype=torch.int32, device=gpu)
+    before = fd.pack(nat.FIELD_POS, rows)
+    src, dst = rows[:1000], rows[2000:3000]
+    fd.set_routes([0], [src], [dst])
+    fd.halo_exchange(comm, nat.FIELD_POS)
+    after = fd.pack(nat.FIELD_POS, rows)
+    torch.testing.assert_close(after[2000:3000], before[:1000], rtol=0, atol=0)
+    torch.testing.assert_close(after[:2000], before[:2000], rtol=0, atol=0)
+    torch.testing.assert_close(after[3000:], before[3000:], rtol=0, atol=0)
+    t64 = torch.tensor([1.5, 2.0, -3.0, 4.0], dtype=torch.float64, device=gpu)
+    comm.allreduce_(t64, nat.OP_SUM)
+    t32 = torch.tensor([7.25], dtype=torch.float32, device=gpu)
+    comm.allreduce_(t32, nat.OP_MAX)
+    torch.cuda.synchronize()
+    assert t64.tolist() == [1.5, 2.0, -3.0, 4.0] and t32.item() == 7.25
 
 
 @pytest.mark.gpu

@@ -41,7 +41,7 @@ def angle(a, b):
     return np.arctan2(s, c)
 
 
-def staged_iteration(pos0, n0, d, dev, k=K, ku=KU, inject_fn=None, inject_pos=None):
+def staged_iteration(pos0, n0, d, dev, k=K, ku=KU, inject_fn=None, inject_pos=None, inject_edge=None):
     """One fused iteration driven stage by stage; returns the per-stage outputs in caller order.
     inject_fn: the reference's smoothed normals, written over K1's f_n before NVT2 (pcd_denoiser_unpack FIELD_FN);
     inject_pos: the reference's positions after phases 0 and 1, written over the current positions before phases 1
@@ -67,6 +67,13 @@ def staged_iteration(pos0, n0, d, dev, k=K, ku=KU, inject_fn=None, inject_pos=No
     out["eig2"] = fd.probe().cpu().numpy()
     rows_all = torch.arange(N, device=dev, dtype=torch.int32)
     perm = grid.perm().long()                           # spatial row -> caller index
+    own_edge = torch.empty((N, 3), device=dev)
+    own_edge[perm] = fd.pack(nat.FIELD_EDGE, rows_all)[:, :3]      # NVT2's own edge vectors, caller order
+    out["edge"] = own_edge.cpu().numpy()
+    if inject_edge is not None:                         # the reference's edge vectors (Processor.py:134) for edge_step
+        e4 = torch.zeros((N, 4), dtype=torch.float32, device=dev)
+        e4[:, :3] = torch.as_tensor(np.ascontiguousarray(inject_edge)).to(dev)[perm]
+        fd.unpack(nat.FIELD_EDGE, rows_all, e4)
     for ph in range(3):
         if inject_pos is not None and ph > 0:
             q4 = torch.zeros((N, 4), dtype=torch.float32, device=dev)
@@ -81,10 +88,10 @@ def staged_iteration(pos0, n0, d, dev, k=K, ku=KU, inject_fn=None, inject_pos=No
         fd.store(q)
         out[f"pos_after_{ph}"] = q.cpu().numpy()
     fd.stage(p, nat.STAGE_FINISH)
-    q, ev = torch.empty((N, 3), device=dev), torch.empty((N, 3), device=dev)
+    q = torch.empty((N, 3), device=dev)
     cls = torch.empty(N, dtype=torch.int64, device=dev)
-    fd.store(q, fn1, cls, ev)                           # n after FINISH = the f_n NVT2 and the phases used
-    out.update(pos=q.cpu().numpy(), f_n=fn1.cpu().numpy(), classes=cls.cpu().numpy(), edge=ev.cpu().numpy(),
+    fd.store(q, fn1, cls)                               # n after FINISH = the f_n NVT2 and the phases used
+    out.update(pos=q.cpu().numpy(), f_n=fn1.cpu().numpy(), classes=cls.cpu().numpy(),
                knn=fd.lists(max(k, ku)).cpu().numpy())
     return out
 
@@ -125,26 +132,44 @@ def check_stages(got, ref_cls, ref_fn, ref_eig2, ref_edge, ref_after, knn, pos0,
     # update neighbours' classes, its own and its neighbours' smoothed normals
     cls_ok = got["classes"] == ref_cls
     nb = knn[:, :KU]
-    dec_ok = cls_ok & cls_ok[nb].all(1) & fn_same & fn_same[nb].all(1) & nb_fn_ok
+    # identical update lists too (the fp32 grid search and the reference's f64 KD-tree order near-ties differently on
+    # a few rows; test_gpu_parity pins the lists themselves)
+    knn_ok = (got["knn"][:, :KU] == nb).all(1)
+    dec_ok = cls_ok & cls_ok[nb].all(1) & fn_same & fn_same[nb].all(1) & nb_fn_ok & knn_ok
+    # the chained variant (own f_n, own edge vectors, own positions after the previous phase) feeds each phase inputs
+    # that differ from the reference's by rounding: a phase's own arithmetic is gated where its CONTINUOUS inputs agree
+    # too (f_n of the point and its update neighbours within 1e-6, input positions within 1e-7 x bbox, edge vector
+    # within 1e-6 rad); the injected variant feeds identical inputs everywhere
+    fn_tight = np.abs(got["f_n"] - ref_fn).max(1) < 1e-6
+    edge_tight = angle(got["edge"], ref_edge) < 1e-6 if not injected else np.ones(len(ref_cls), bool)
+    prev = [pos0] + list(ref_after)
     stats = {}
     for ph in range(3):
         dev_ = np.linalg.norm(got[f"pos_after_{ph}"] - ref_after[ph], axis=1) / bbox
         moved = ref_cls == ph
-        m = dec_ok & moved
+        inp = got[f"pos_after_{ph - 1}"] if ph > 0 else pos0
+        pos_tight = np.linalg.norm(inp - prev[ph], axis=1) / bbox < 1e-7
+        tight = fn_tight & fn_tight[nb].all(1) & pos_tight & pos_tight[nb].all(1)
+        if ph == 1:
+            tight &= edge_tight
+        m = dec_ok & moved & (tight if not injected else True)
         stats[ph] = (float(dev_[m].max()), float(np.percentile(dev_[m], 99)), float(np.percentile(dev_[m], 99.9)),
-                     float(1 - dec_ok[moved].mean()))
-        # The flat step returns v + di (rounding relative to the small move): 1e-6 x bbox at p99.9.
-        # The edge and feature steps return the solution x of a 3x3 system in ABSOLUTE coordinates, so fp32 rounding
-        # scales with |x| cond(A) eps -- the reference inverts A (inv_ex, then A^-1 b), the kernels solve by LU:
-        # p99 <= 2e-6, p99.9 <= 3e-6 x bbox.  Measured: the library built with NVT2 on the LAPACK
-        # ssyevd restatement (PCD_NVT2_LAPACK) shows the same 1.4-2.2e-6 at p99.9 in the edge phase as the shipped
-        # Jacobi, with every phase fed the reference's own inputs -- the steps' conditioning, not the solver.
-        assert np.percentile(dev_[m], 99.9) <= (1e-6 if ph == 0 else 3e-6), (label, ph, stats[ph])
-        assert np.percentile(dev_[m], 99) <= (1e-6 if ph == 0 else 2e-6), (label, ph, stats[ph])
+                     float(1 - dec_ok[moved].mean()), float(1 - m.sum() / max(moved.sum(), 1)))
         if ph == 0:
             assert (dev_[dec_ok & ~moved] == 0).all(), (label, ph)   # the flat phase copies the others
+    print(label, "excluded", round(float(excl), 5), "eig max", float(e.max()),
+          "phases (max, p99, p99.9, decisions differ, excluded)", stats)
+    # SURVEY §8(c)'s single-step gate (identical inputs): <= 1e-6 x bbox, every phase.  The edge / feature / corner
+    # steps restate the reference's inv_ex (MKL getrf(Aᵀ) + getrs('T'), bitwise:
+    # test_capi.py::test_host_inv3_matches_torch_bitwise), its einsum products and its list-order sums; the flat step
+    # differs only in the global centre's summation order (f64 here, a float32 torch mean there).
+    # The chained variant's edge vectors come from NVT2's own solver (within 5e-7 / gap of LAPACK's,
+    # test_nvt2_jacobi_matches_lapack_restatement) and move the edge step's x by up to |x| times that angle: its gate
+    # is 3e-6 x bbox, still two orders inside §8(c)'s one-iteration end-to-end gate (p99 3e-4 x bbox).
+    for ph in range(3):
+        assert stats[ph][2] <= (1e-6 if injected else 3e-6), (label, ph, stats[ph])
+        assert stats[ph][4] < (0.02 if injected else 0.8), (label, ph, stats[ph])
     assert dec_ok.mean() > (0.99 if injected else 0.90), (label, dec_ok.mean())
-    print(label, "excluded", round(float(excl), 5), "eig max", float(e.max()), "phases (max, p99, p99.9, excluded)", stats)
     return stats
 
 
@@ -154,11 +179,15 @@ def test_fused_stages_match_reference_fixture(golden, gpu, injected):
     f = golden("fandisk_k32")
     ref_after = [f["it1_pos_after_0"], f["it1_pos_after_1"], f["it1_pos_after_2"]]
     got = staged_iteration(f["pos0"], f["n0"], float(f["d"]), gpu, inject_fn=f["it1_f_n"] if injected else None,
-                           inject_pos=ref_after if injected else None)
+                           inject_pos=ref_after if injected else None,
+                           inject_edge=f["it1_eigvec2"][..., 0] if injected else None)
     # the kNN list the loop used IS the reference's (frozen snapshot, current = snapshot positions at iteration 1)
     assert (got["knn"][:, :K] == f["knn32"]).mean() > 0.999
-    check_stages(got, f["it1_classes"], f["it1_f_n"], f["it1_eigval2"], f["it1_eigvec2"][..., 0], ref_after,
-                 f["knn32"], f["pos0"], "fandisk", injected)
+    stats = check_stages(got, f["it1_classes"], f["it1_f_n"], f["it1_eigval2"], f["it1_eigvec2"][..., 0], ref_after,
+                         f["knn32"], f["pos0"], "fandisk", injected)
+    if injected:
+        # identical inputs: the edge and feature steps are the reference's own arithmetic, bit for bit
+        assert stats[1][0] == 0.0 and stats[2][0] == 0.0, stats
 
 
 @pytest.mark.parametrize("injected", [True, False], ids=["oracle_fn", "own_fn"])
@@ -174,7 +203,8 @@ def test_fused_stages_match_oracle_headline_sample(gpu, injected):
     O.denoise_iteration(p0, n0, knn, d, K, KU, record=rec)
     ref_after = [rec["pos_after_0"], rec["pos_after_1"], rec["pos_after_2"]]
     got = staged_iteration(p0, n0, d, gpu, inject_fn=rec["f_n"] if injected else None,
-                           inject_pos=ref_after if injected else None)
+                           inject_pos=ref_after if injected else None,
+                           inject_edge=rec["edge_vectors"] if injected else None)
     assert (got["knn"][:, :K] == rec["knn"]).mean() > 0.999
     check_stages(got, rec["classes"], rec["f_n"], rec["eigval2"], rec["edge_vectors"], ref_after, rec["knn"], p0,
                  "headline-200k", injected)

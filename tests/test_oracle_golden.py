@@ -120,9 +120,14 @@ def test_denoiser_steps(steps, kind, alpha):
         else:
             out = O.STEPS[kind](pos, n1, sub, nbr, dd, alpha)
         dev = np.linalg.norm(out - steps[key], axis=1) / bbox
-        # ill-conditioned 3x3 solves amplify fp32 rounding: gate the bulk tightly, allow a small tail
-        assert np.percentile(dev, 95) < 1e-5, (key, np.percentile(dev, 95))
-        assert (dev < 1e-3).mean() > 0.99, key
+        if kind in ("edge", "feature", "corner"):
+            # the solve steps are restated op for op (torch's inv_ex and einsum, the same sums in list order): the
+            # reference's own output bit for bit
+            np.testing.assert_array_equal(out, steps[key], err_msg=key)
+            continue
+        # flat / new: the global centre is an f64 mean here, a float32 torch mean (cascade summation) there
+        assert np.percentile(dev, 99.9) < 1e-5, (key, np.percentile(dev, 99.9))
+        assert dev.max() < 1e-5, (key, dev.max())
 
 
 def test_dummy_step(steps):
@@ -208,3 +213,22 @@ def angle64(a, b):
     """Angle between row vectors in float64 (arccos of an f32 dot cannot resolve below ~5e-4 rad)."""
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
     return np.arctan2(np.linalg.norm(np.cross(a, b), axis=1), (a * b).sum(1))
+
+
+def test_cpsd_driver_oracle_matches_reference(golden):
+    """pcd_oracle.cpsd_iteration (the CPSD driver's loop body, PostProcessing.ipynb:1041-1062) against the reference's
+    own run of that loop on fandisk (cpsd.npz drv_*): iteration 1 at the single-iteration gates (median exact, p99
+    1e-5 x bbox), iteration 2 within the chaotic envelope of SURVEY §8(c)."""
+    c = golden("cpsd")
+    pos0, n0, d = c["pos"], c["n"], float(c["drv_d"])
+    bbox = float(np.linalg.norm(pos0.max(0) - pos0.min(0)))
+    knn = O.FrozenKNN(pos0)
+    rp, rn = pos0.copy(), n0.copy()
+    for it in (1, 2):
+        rp, rn = O.cpsd_iteration(pos0, rp, rn, pos0, knn, d)
+        dev = np.linalg.norm(rp - c[f"drv_pos_it{it}"], axis=1) / bbox
+        if it == 1:
+            assert np.median(dev) < 1e-7 and np.percentile(dev, 99) < 1e-5 and dev.max() < 1e-4, dev.max()
+            assert np.abs(rn - c["drv_n_it1"]).max() < 1e-6
+        else:
+            assert np.median(dev) < 1e-5 and np.percentile(dev, 99) < 5e-3, np.percentile(dev, 99)

@@ -182,6 +182,16 @@ def test_slab_world2_rebalance_by_cost_matches_oracle(tmp_path):
     _assert_matches_oracle(res)
 
 
+def test_slab_world2_rebalance_verifies_pending_iterations(tmp_path):
+    """rebalance() in the middle of a check window (check_every=2, one unchecked iteration) on a thin halo: the
+    pending iterations are verified first -- the coverage miss re-plans and replays them -- so the state carried into
+    the cost-weighted cut is exact and the run still equals the oracle's."""
+    res = _run_world2(tmp_path, 0.05, {"check_every": 2, "halo_growth": 3.0, "rebalance_after": 1})
+    assert int(res["err"]) == 0
+    assert int(res["replans"]) >= 1
+    _assert_matches_oracle(res)
+
+
 def test_plan_weighted_cut():
     pos, _ = _cloud()
     w = torch.ones(pos.size(0), dtype=torch.float32)
