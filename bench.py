@@ -223,30 +223,60 @@ def mesh_bench(dev, cpu):
     return out
 
 
-def cpsd_bench(dev, cpu, points=50_000, iterations=50):
-    """The CPSD ("Martin") 50-iteration driver (PostProcessing.ipynb:1041-1062, Processor.cpsdDenoise) on a 50k-point
-    bunny-sampled cloud: seconds per iteration against the reference's 1.13 s/it on the 50k-point Stitch_guitar
-    (PostProcessing.ipynb:1015, author's CPU)."""
-    pos, nrm, _ = make_cloud(points, 4, dev)
-    proc = Processor(Pointcloud(pos.clone(), nrm.clone()), k_hint=16)
-    d = 2 * float(proc.meanEdgeLength())
-    proc.cpsdDenoise(iterations=1, d=d)                  # warm-up (allocations, kernels)
-    proc = Processor(Pointcloud(pos.clone(), nrm.clone()), k_hint=16)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    proc.cpsdDenoise(iterations=iterations, d=d)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / iterations
-    out = {"points": points, "iterations": iterations, "s_per_iteration": round(dt, 6),
-           "reference_s_per_iteration": 1.13, "reference_source": "PostProcessing.ipynb:1015 (50k-point Stitch_guitar, "
-           "author's CPU)", "speedup_vs_reference": round(1.13 / dt, 1)}
-    if cpu:
-        from oracle import pcd_oracle as O
-        p0, n0 = pos.cpu().numpy(), nrm.cpu().numpy()
-        knn = O.FrozenKNN(p0)
+def cpsd_alg_bytes(m, ku=8):
+    """Algorithmic bytes / point / iteration of the fused CPSD driver (pcd_cpsd_iterate), SURVEY §8(d)'s convention
+    (every neighbour attribute read counted per use, f32 values, int32 indices), m = mean radius members:
+      kNN(k_u) lists       12 + 12 k_u + 4 k_u
+      radius NVT + VU      12 (own pos) + 12 m (member xyz) + 12 m (n_j) + 12 (own n) + 12 (f_n) + 4 m (member rows)
+      PVT + VU features    4 m (rows) + 24 (own pos, f_n) + 3 x 12 m (f_n_j: the vote, and again in the two sums)
+                           + 2 x 12 m (v_j: centroid and covariance) + 13 (class, edge vector)
+      phases (Jacobi)      flat reduce 2 (4 + 16 k_u) + update 4 + 4 k_u + 36 + 24 k_u + 12 (+ 16: the global clamp's orig)"""
+    knn = 12 + 16 * ku
+    nvt = 36 + 28 * m
+    pvt = 37 + 64 * m
+    phases = 2 * (4 + 16 * ku) + 4 + 28 * ku + 48 + 16
+    return knn + nvt + pvt + phases
+
+
+def cpsd_bench(dev, cpu, sizes=(50_000, 1_000_000), iterations=50):
+    """The CPSD ("Martin") 50-iteration driver (PostProcessing.ipynb:1041-1062, Processor.cpsdDenoise -> one
+    pcd_cpsd_iterate call) on bunny-sampled clouds: seconds per iteration against the reference's 1.13 s/it on the
+    50k-point Stitch_guitar (PostProcessing.ipynb:1015, author's CPU), and at 1M points a roofline on
+    cpsd_alg_bytes."""
+    out = {"reference_s_per_iteration": 1.13, "reference_source": "PostProcessing.ipynb:1015 (50k-point Stitch_guitar, "
+           "author's CPU)", "iterations": iterations}
+    for points in sizes:
+        pos, nrm, _ = make_cloud(points, 4, dev)
+        proc = Processor(Pointcloud(pos.clone(), nrm.clone()), k_hint=16)
+        d = 2 * float(proc.meanEdgeLength())
+        m = float(proc.selector.getPointsInRangeSelection(d).slices.diff().float().mean())
+        proc.cpsdDenoise(iterations=2, d=d)                  # warm-up (allocations, list slots, kernels)
+        proc.pointcloud.v.copy_(pos)
+        proc.graph.n = nrm.clone()
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
-        O.cpsd_iteration(p0, p0, n0, p0, knn, d)
-        out["cpu_oracle_s_per_iteration"] = round(time.perf_counter() - t0, 4)
+        proc.cpsdDenoise(iterations=iterations, d=d)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / iterations
+        row = {"points": points, "s_per_iteration": round(dt, 6), "mean_members": round(m, 2)}
+        if points == 50_000:
+            row["speedup_vs_reference"] = round(1.13 / dt, 1)
+            if cpu:
+                from oracle import pcd_oracle as O
+                p0, n0 = pos.cpu().numpy(), nrm.cpu().numpy()
+                knn = O.FrozenKNN(p0)
+                t1 = time.perf_counter()
+                O.cpsd_iteration(p0, p0, n0, p0, knn, d)
+                row["cpu_oracle_s_per_iteration"] = round(time.perf_counter() - t1, 4)
+        b = cpsd_alg_bytes(m) * points
+        row["roofline"] = {"bound": "valu+latency", "alg_bytes_per_point": round(cpsd_alg_bytes(m), 1),
+                           "achieved": round(b / dt / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(b / dt / 1e9 / HBM_PEAK_GBS, 4)}
+        out[f"n{points // 1000}k"] = row
+    if "n50k" in out:          # (the round-3 keys, kept)
+        out["points"] = 50_000
+        out["s_per_iteration"] = out["n50k"]["s_per_iteration"]
+        out["speedup_vs_reference"] = out["n50k"].get("speedup_vs_reference")
     return out
 
 

@@ -364,6 +364,10 @@ int pcd_host_solve3(const float* a9, const float* b3, int64_t m, float* x3, int3
 /* torch.linalg.inv_ex (Denoiser.py:43, 80, 163, 210) restated for 3x3: a9 [m][3][3] -> inv9 [m][3][3], ok [m] as
  * above (inv untouched = 0 where ok = 0).  The position steps' arithmetic (pcd_device.h inv3_ref), on the host. */
 int pcd_host_inv3(const float* a9, int64_t m, float* inv9, int32_t* ok);
+/* Denoiser.*_step (PCD_STEP_*) over CSR rows, the kernels' step functions on the host: out [m][3]; delta = the global
+ * flat / new-step delta (Denoiser.py:107, 138). */
+int pcd_host_step_csr(int kind, const float* pos, const float* n, const float* edge_vectors, const int64_t* ci,
+                      const int64_t* off, const int64_t* nbr, int64_t m, float delta, float d, float alpha, float* out);
 
 #ifdef __cplusplus
 }

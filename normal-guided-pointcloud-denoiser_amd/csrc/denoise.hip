@@ -298,13 +298,30 @@ PCD_DEV bool anchor_holds(float d2k, Vec3 q, float4 a) {
 #define PCD_ANCHOR_BS 128
 #endif
 static constexpr int kAnchorBS = PCD_ANCHOR_BS;
+#ifndef PCD_ANCHOR_OCC
+#define PCD_ANCHOR_OCC 1
+#endif
+// The slot -> rank map in LDS as 24-bit offsets from the set's first (smallest) rank: 192 B a lane instead of 256,
+// room for 3 waves per SIMD instead of 2 (a set whose ranks span 2^24 or more -- only past 16M points, at the top
+// Morton boundaries -- fails the test and is re-anchored exactly).
+#ifndef PCD_ANCHOR_MAP24
+#define PCD_ANCHOR_MAP24 0
+#endif
+#ifndef PCD_ANCHOR_BATCH
+#define PCD_ANCHOR_BATCH 64   // anchor-set slots gathered per batch (all of them by default)
+#endif
 template <int K, int KA>
-__global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const float4* __restrict__ pos, int64_t N,
+__global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridView g, const float4* __restrict__ pos, int64_t N,
                                                           RowMap rm, int kstore, const float4* __restrict__ anc,
                                                           const int32_t* __restrict__ alist,
                                                           int32_t* __restrict__ idx, uint8_t* __restrict__ fail) {
     static_assert(KA == 2 * K && KA <= 64, "anchor lists hold twice the list cap; 6 slot bits");
+#if PCD_ANCHOR_MAP24
+    __shared__ uint16_t s_lo[KA * kAnchorBS];
+    __shared__ uint8_t s_hi[KA * kAnchorBS];
+#else
     __shared__ uint32_t s_r[KA * kAnchorBS];
+#endif
     const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * kAnchorBS + threadIdx.x;
     bool failed = false;
     if (t0 < rm.nq) {
@@ -323,28 +340,57 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
             // every list point is within D of the anchor, hence within D + delta of q
             const float R = (a.w + delta) * (1.f + 1e-5f);
             const float S = 67108864.f / fmaxf(R * R, 1e-30f);
-            uint32_t r[KA], c[KA];
-            {
-                int rl[KA];
-                load_list<KA, true>(alist, N, i, KA, rl);
-#pragma unroll
-                for (int t = 0; t < KA; ++t) r[t] = (uint32_t)rl[t];
-            }
+            uint32_t c[KA];
             int below = 0;
+            // the set's ranks and rows in batches of AB slots (AB = KA: every gather in flight at once; a smaller batch
+            // holds fewer rows in registers, a scheduling barrier keeping the next batch's loads behind this one's keys)
+            constexpr int AB = PCD_ANCHOR_BATCH < KA ? PCD_ANCHOR_BATCH : KA;
+            static_assert(KA % AB == 0 && AB % 8 == 0, "whole 8-column blocks per batch");
+#if PCD_ANCHOR_MAP24
+            uint32_t base = 0;
+            bool span_ok = true;
+#endif
 #pragma unroll
-            for (int t = 0; t < KA; ++t) {
-                // an unused slot of a partial anchor set holds N: the snapshot's +inf sentinel row (the min keeps any
-                // entry inside the allocation)
-                const uint32_t rt = min(r[t], (uint32_t)N);
-                s_r[t * kAnchorBS + threadIdx.x] = rt;
-                const float d2 = dist2(vi, *at32(g.pts, rt));   // unconditional load: all KA gathers in flight
-                below += d2 < T ? 1 : 0;
-                // clamp below 2^26 in fp32 (2^26 - 1 rounds UP to 2^26, which would wrap to 0 after the shift);
-                // only the sentinel's infinite distance reaches it
-                c[t] = ((uint32_t)fminf(d2 * S, 67108860.f) << 6) | (uint32_t)t;
+            for (int b0 = 0; b0 < KA; b0 += AB) {
+                uint32_t r[AB];
+#pragma unroll
+                for (int g8 = 0; g8 < AB / 8; ++g8) {
+                    const v4i* lp = lblock(alist, N, i, b0 / 8 + g8);
+                    const v4i x = __builtin_nontemporal_load(lp), y = __builtin_nontemporal_load(lp + 1);
+                    r[8 * g8 + 0] = (uint32_t)x.x; r[8 * g8 + 1] = (uint32_t)x.y; r[8 * g8 + 2] = (uint32_t)x.z;
+                    r[8 * g8 + 3] = (uint32_t)x.w; r[8 * g8 + 4] = (uint32_t)y.x; r[8 * g8 + 5] = (uint32_t)y.y;
+                    r[8 * g8 + 6] = (uint32_t)y.z; r[8 * g8 + 7] = (uint32_t)y.w;
+                }
+#if PCD_ANCHOR_MAP24
+                if (b0 == 0) base = min(r[0], (uint32_t)N);   // (the set is stored in rank order: its smallest rank)
+#endif
+#pragma unroll
+                for (int u = 0; u < AB; ++u) {
+                    const int t = b0 + u;
+                    // an unused slot of a partial anchor set holds N: the snapshot's +inf sentinel row (the min keeps
+                    // any entry inside the allocation)
+                    const uint32_t rt = min(r[u], (uint32_t)N);
+#if PCD_ANCHOR_MAP24
+                    const uint32_t dl = rt - base;
+                    span_ok = span_ok && dl < (1u << 24);
+                    s_lo[t * kAnchorBS + threadIdx.x] = (uint16_t)dl;
+                    s_hi[t * kAnchorBS + threadIdx.x] = (uint8_t)(dl >> 16);
+#else
+                    s_r[t * kAnchorBS + threadIdx.x] = rt;
+#endif
+                    const float d2 = dist2(vi, *at32(g.pts, rt));   // unconditional load: the batch's gathers in flight
+                    below += d2 < T ? 1 : 0;
+                    // clamp below 2^26 in fp32 (2^26 - 1 rounds UP to 2^26, which would wrap to 0 after the shift);
+                    // only the sentinel's infinite distance reaches it
+                    c[t] = ((uint32_t)fminf(d2 * S, 67108860.f) << 6) | (uint32_t)t;
+                }
+                if (AB < KA) __builtin_amdgcn_sched_barrier(0);
             }
             PCD_ANCHOR_SORT<KA>(c);
             bool ok = below >= kstore;
+#if PCD_ANCHOR_MAP24
+            ok = ok && span_ok;
+#endif
 #pragma unroll
             for (int t = 0; t < K; ++t)
                 if (t < kstore) ok = ok && (c[t] >> 6) < (c[t + 1] >> 6);
@@ -352,7 +398,14 @@ __global__ __launch_bounds__(kAnchorBS) void k_knn_anchor(GridView g, const floa
             if (ok) {
                 int out[K];
 #pragma unroll
-                for (int t = 0; t < K; ++t) out[t] = (int32_t)s_r[(c[t] & 63u) * kAnchorBS + threadIdx.x];
+                for (int t = 0; t < K; ++t) {
+#if PCD_ANCHOR_MAP24
+                    const uint32_t sl = (c[t] & 63u) * kAnchorBS + threadIdx.x;
+                    out[t] = (int32_t)(base + (((uint32_t)s_hi[sl] << 16) | (uint32_t)s_lo[sl]));
+#else
+                    out[t] = (int32_t)s_r[(c[t] & 63u) * kAnchorBS + threadIdx.x];
+#endif
+                }
                 store_list<K, true>(idx, N, i, kstore, out);
             }
         }
@@ -941,9 +994,9 @@ struct pcd_denoiser {
     bool xpending = false;        // xev_out marks an exchange the state's next reader must wait for
     bool xbegun = false;          // host transport: packed, callback not yet run
     XField xfield{};
-    // CPSD driver (pcd_cpsd.h): radius lists [N][cpsd_cap] of (original index << 32 | row), member counts, overflow
+    // CPSD driver (pcd_cpsd.h): radius member rows, member counts, overflow flag
     bool nvt1_on = true;          // K1 runs NVT1 after the kNN (off: the lists only)
-    unsigned long long* ckeys = nullptr;
+    int32_t* ckeys = nullptr;                            // [N][cpsd_cap] member rows, ascending original index
     int32_t* ccnt = nullptr;
     int* covf = nullptr;
     int cpsd_cap = 0;

@@ -70,6 +70,30 @@ int pcd_host_inv3(const float* a9, int64_t m, float* inv9, int32_t* ok) {
     return PCD_OK;
 }
 
+int pcd_host_step_csr(int kind, const float* pos, const float* n, const float* edge_vectors, const int64_t* ci,
+                      const int64_t* off, const int64_t* nbr, int64_t m, float delta, float d, float alpha, float* out) {
+    PCD_CHECK_ARG(pos && n && ci && off && (m == 0 || nbr) && out, "null argument");
+    PCD_CHECK_ARG(kind != PCD_STEP_EDGE || edge_vectors, "edge_step needs edge vectors");
+    const Rows3 P{pos}, N{n};
+    for (int64_t r = 0; r < m; ++r) {
+        const int64_t c = ci[r];
+        const int cnt = (int)(off[r + 1] - off[r]);
+        const HostCsrNb nb{nbr, off[r]};
+        const Vec3 vi = P(c);
+        Vec3 o;
+        switch (kind) {
+            case PCD_STEP_FLAT: o = step_flat(P, N, vi, N(c), cnt, nb, delta, d, alpha); break;
+            case PCD_STEP_EDGE: o = step_edge(P, N, vi, Rows3{edge_vectors}(c), cnt, nb, d, alpha); break;
+            case PCD_STEP_FEATURE: o = step_feature<false>(P, N, vi, N(c), cnt, nb, 1.f, d, alpha); break;
+            case PCD_STEP_NEW: o = step_feature<true>(P, N, vi, N(c), cnt, nb, delta, d, alpha); break;
+            case PCD_STEP_CORNER: o = step_corner(P, N, vi, cnt, nb, d, alpha); break;
+            default: o = vi; break;
+        }
+        out[3 * r] = o.x; out[3 * r + 1] = o.y; out[3 * r + 2] = o.z;
+    }
+    return PCD_OK;
+}
+
 int pcd_host_nvt_tensor(const float* pos, const float* n, const int64_t* ci, const int64_t* off, const int64_t* nbr,
                         int64_t m, float rho, float* t6) {
     PCD_CHECK_ARG(pos && n && ci && off && (m == 0 || nbr) && t6, "null argument");

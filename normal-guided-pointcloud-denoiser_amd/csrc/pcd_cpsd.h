@@ -13,7 +13,7 @@
 //               (temp_pos = pos.clone()), per-step clamp d * 20000, global clamp ||temp_pos - original_pos|| < d
 //               (the fused loop's jacobi + clamp_global phases, Denoiser.py:26-119)
 //   n := f_n
-// Radius lists live in [N][cap] slots of 64-bit keys (original index << 32 | snapshot row), sorted per row in place.
+// Radius members are collected and sorted in LDS (cap slots a lane, 16 / 32 / 64 / 128) and stored as [N][cap] rows.
 // A row with more than cap members raises a device flag; the call checks it once at the end (its only host sync) and,
 // if set, restores the state it started from, doubles cap and runs again -- results never depend on cap.
 
@@ -21,25 +21,33 @@ namespace pcd {
 
 static constexpr int kCpsdBS = 128;
 
-// Members of row i's list in ascending original index (the keys' row halves).
-struct KeyNb {
-    const unsigned long long* L;
-    PCD_DEV int64_t operator()(int t) const { return (int64_t)(uint32_t)(L[t] & 0xFFFFFFFFull); }
+// Members of a row's list in ascending original index (the keys' row halves), read from the lane's LDS slots.
+struct LdsKeyNb {
+    const unsigned long long* L;    // this lane's slot 0; slot t at L[t * BS]
+    int bs;
+    PCD_DEV int64_t operator()(int t) const { return (int64_t)(uint32_t)(L[t * bs] & 0xFFFFFFFFull); }
+};
+struct RowNb {
+    const int32_t* L;
+    PCD_DEV int64_t operator()(int t) const { return L[t]; }
 };
 
-// Radius selection + normal-filtered NVT + VU smoothing of each active row.
-__global__ __launch_bounds__(kCpsdBS) void k_cpsd_nvt(GridView g, const float4* __restrict__ pos,
-                                                      const float4* __restrict__ nrm, int64_t N, RowMap rm, float r,
-                                                      float rho, float tau, float damp,
-                                                      unsigned long long* __restrict__ keys, int cap,
-                                                      int32_t* __restrict__ cnt, float4* __restrict__ fn,
-                                                      int* __restrict__ ovf) {
-    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * kCpsdBS + threadIdx.x;
+// Radius selection + normal-filtered NVT + VU smoothing of each active row.  The members are collected as
+// (original index << 32 | row) keys in the lane's CAP LDS slots (slot-major: conflict-free), insertion-sorted there
+// (a few dozen LDS round trips, not global ones), summed in that order, and their rows stored for the PVT pass.
+template <int CAP, int BS>
+__global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __restrict__ pos,
+                                                 const float4* __restrict__ nrm, int64_t N, RowMap rm, float r,
+                                                 float rho, float tau, float damp, int32_t* __restrict__ rows,
+                                                 int32_t* __restrict__ cnt, float4* __restrict__ fn,
+                                                 int* __restrict__ ovf) {
+    __shared__ unsigned long long s_k[CAP * BS];
+    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * BS + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 q4 = pos[i];
     const float qx = q4.x, qy = q4.y, qz = q4.z;
-    unsigned long long* L = keys + (size_t)i * (size_t)cap;
+    unsigned long long* L = s_k + threadIdx.x;
     int m = 0;
     const double rd = (double)r, r2 = rd * rd;
     if (rd >= 0.0) {
@@ -62,27 +70,33 @@ __global__ __launch_bounds__(kCpsdBS) void k_cpsd_nvt(GridView g, const float4* 
                                      dz = (double)qz - (double)p.z;
                         const double d2 = __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
                         if (d2 <= r2) {
-                            if (m < cap) L[m] = ((unsigned long long)__float_as_uint(p.w) << 32) | r0;
+                            if (m < CAP) L[m * BS] = ((unsigned long long)__float_as_uint(p.w) << 32) | r0;
                             ++m;
                         }
                     }
                 }
     }
     cnt[i] = m;
-    if (m > cap) {          // (the call replays with a larger cap; this row's result is discarded)
+    if (m > CAP) {          // (the call replays with more slots; this row's result is discarded)
         atomicOr(ovf, 1);
-        m = cap;
+        m = CAP;
     }
     // ascending original index: scipy's per-query order, the order the reference's scatter sums in
     for (int a = 1; a < m; ++a) {
-        const unsigned long long k = L[a];
+        const unsigned long long k = L[a * BS];
         int b = a - 1;
-        while (b >= 0 && L[b] > k) { L[b + 1] = L[b]; --b; }
-        L[b + 1] = k;
+        for (; b >= 0; --b) {
+            const unsigned long long kb = L[b * BS];
+            if (kb <= k) break;
+            L[(b + 1) * BS] = kb;
+        }
+        L[(b + 1) * BS] = k;
     }
+    int32_t* R = rows + (size_t)i * CAP;
+    for (int t = 0; t < m; ++t) R[t] = (int32_t)(uint32_t)(L[t * BS] & 0xFFFFFFFFull);
     const float4 n4 = nrm[i];
     const Vec3 ni = v3(n4.x, n4.y, n4.z);
-    const Sym3 T = nvt_normal_tensor(Rows4{nrm}, ni, m, KeyNb{L}, rho);
+    const Sym3 T = nvt_normal_tensor(Rows4{nrm}, ni, m, LdsKeyNb{L, BS}, rho);
     float w[3], V[3][3];
     eigh3(T, w, V);
     const Vec3 f = vu_smooth(w, V, ni, tau, damp);
@@ -92,7 +106,7 @@ __global__ __launch_bounds__(kCpsdBS) void k_cpsd_nvt(GridView g, const float4* 
 // Normal-filtered PVT on f_n over the same members, eigh, VU features + edge vector of each active row.
 __global__ __launch_bounds__(kCpsdBS) void k_cpsd_pvt(const float4* __restrict__ pos, const float4* __restrict__ fn,
                                                       int64_t N, RowMap rm, float rho, float tau,
-                                                      const unsigned long long* __restrict__ keys, int cap,
+                                                      const int32_t* __restrict__ rows, int cap,
                                                       const int32_t* __restrict__ cnt, uint8_t* __restrict__ cls,
                                                       float4* __restrict__ edge) {
     const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * kCpsdBS + threadIdx.x;
@@ -101,13 +115,21 @@ __global__ __launch_bounds__(kCpsdBS) void k_cpsd_pvt(const float4* __restrict__
     const int m = min(cnt[i], cap);
     const float4 p4 = pos[i], f4 = fn[i];
     const Sym3 C = pvt_normal_cov(Rows4{pos}, Rows4{fn}, v3(p4.x, p4.y, p4.z), v3(f4.x, f4.y, f4.z), m,
-                                  KeyNb{keys + (size_t)i * (size_t)cap}, rho);
+                                  RowNb{rows + (size_t)i * cap}, rho);
     float w[3], V[3][3];
     eigh3(C, w, V);
     // getVUFeatures(tau) = (eigval < tau).sum(dim=1) % 3 (Decompositionor.py:84-85); NaN compares false
     const int below = (w[0] < tau ? 1 : 0) + (w[1] < tau ? 1 : 0) + (w[2] < tau ? 1 : 0);
     cls[i] = (uint8_t)(below % 3);
     edge[i] = make_float4(V[0][0], V[1][0], V[2][0], 0.f);   // eigvec[..., 0] (Processor's edge_vectors)
+}
+
+__global__ void k_cpsd_maxcnt(const int32_t* __restrict__ cnt, RowMap rm, int* __restrict__ mx) {
+    int v = 0;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < rm.nq; t += (int64_t)gridDim.x * blockDim.x)
+        v = max(v, cnt[rm(t)]);
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(mx, v);
 }
 
 }  // namespace pcd
@@ -125,7 +147,7 @@ static int cpsd_alloc(pcd_denoiser* dn, int cap) {
     (void)hipFree(dn->ckeys);
     dn->ckeys = nullptr;
     dn->cpsd_cap = 0;
-    if (hipMalloc(&dn->ckeys, (size_t)N * (size_t)cap * sizeof(unsigned long long)) != hipSuccess)
+    if (hipMalloc(&dn->ckeys, (size_t)N * (size_t)cap * sizeof(int32_t)) != hipSuccess)
         return fail(PCD_ERR_OOM, "pcd_cpsd_iterate: radius lists");
     if (!dn->ccnt && (hipMalloc(&dn->ccnt, N * sizeof(int32_t)) != hipSuccess ||
                       hipMalloc(&dn->covf, sizeof(int)) != hipSuccess ||
@@ -158,7 +180,7 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
     p.jacobi = 1;
     p.clamp_global = cp->d;
     if ((rc = check_params(dn, &p)) != PCD_OK) return rc;
-    if (dn->cpsd_cap == 0 && (rc = cpsd_alloc(dn, 32)) != PCD_OK) return rc;
+    if (dn->cpsd_cap == 0 && (rc = cpsd_alloc(dn, 16)) != PCD_OK) return rc;
     const int64_t N = dn->n;
     const RowMap rm = dn->rowmap();
     // the state this call starts from (a replay after a radius-list overflow restarts from it)
@@ -166,7 +188,7 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
     PCD_HIP(hipMemcpyAsync(dn->csave_nrm, dn->nrm, N * sizeof(float4), hipMemcpyDeviceToDevice, st));
     const int cur0 = dn->cur;
     const bool unit0 = dn->unit_nrm;
-    for (int attempt = 0;; ++attempt) {
+    for (;;) {
         PCD_HIP(hipMemsetAsync(dn->covf, 0, sizeof(int), st));
         dn->nvt1_on = false;
         for (int it = 0; it < iterations && rc == PCD_OK; ++it) {
@@ -175,10 +197,17 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
             const GridView gv = dn->g->view;
             const dim3 grd((unsigned)cdiv(rm.nq, kCpsdBS)), blk(kCpsdBS);
             if (rm.nq > 0) {
-                hipLaunchKernelGGL(k_cpsd_nvt, grd, blk, 0, st, gv, dn->pos[dn->cur], dn->nrm, N, rm, cp->r, cp->rho,
-                                   cp->tau, cp->damp, dn->ckeys, dn->cpsd_cap, dn->ccnt, dn->fn, dn->covf);
+                const int cap = dn->cpsd_cap;
+#define PCD_CPSD_NVT(C, B)                                                                                             \
+    hipLaunchKernelGGL((k_cpsd_nvt<C, B>), dim3((unsigned)cdiv(rm.nq, B)), dim3(B), 0, st, gv, dn->pos[dn->cur], dn->nrm, \
+                       N, rm, cp->r, cp->rho, cp->tau, cp->damp, dn->ckeys, dn->ccnt, dn->fn, dn->covf)
+                if (cap == 16) PCD_CPSD_NVT(16, 128);
+                else if (cap == 32) PCD_CPSD_NVT(32, 128);
+                else if (cap == 64) PCD_CPSD_NVT(64, 64);
+                else PCD_CPSD_NVT(128, 64);
+#undef PCD_CPSD_NVT
                 hipLaunchKernelGGL(k_cpsd_pvt, grd, blk, 0, st, dn->pos[dn->cur], dn->fn, N, rm, cp->rho, cp->tau,
-                                   dn->ckeys, dn->cpsd_cap, dn->ccnt, dn->cls, dn->edge);
+                                   dn->ckeys, cap, dn->ccnt, dn->cls, dn->edge);
                 if (hipGetLastError() != hipSuccess) { rc = fail(PCD_ERR_HIP, "pcd_cpsd_iterate: launch"); break; }
             }
             for (int ph = 0; ph < 3 && rc == PCD_OK; ++ph) {
@@ -197,10 +226,29 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
         int ovf = 0;
         PCD_HIP(hipMemcpyAsync(&ovf, dn->covf, sizeof(int), hipMemcpyDeviceToHost, st));
         PCD_HIP(hipStreamSynchronize(st));
-        if (!ovf || iterations == 0) break;
+        if (!ovf || iterations == 0) {
+            // slots for the next call with headroom: the largest selection of the last iteration above 3/4 of the
+            // slots doubles them now, so a later call does not replay when the points drift into denser spots
+            if (iterations > 0 && dn->cpsd_cap < 128 && rm.nq > 0) {
+                int* mx = dn->covf;                       // (reused as the max-count cell)
+                PCD_HIP(hipMemsetAsync(mx, 0, sizeof(int), st));
+                hipLaunchKernelGGL(k_cpsd_maxcnt, dim3((unsigned)std::min<int64_t>(cdiv(rm.nq, 256), 1024)), dim3(256),
+                                   0, st, dn->ccnt, rm, mx);
+                int h = 0;
+                PCD_HIP(hipMemcpyAsync(&h, mx, sizeof(int), hipMemcpyDeviceToHost, st));
+                PCD_HIP(hipStreamSynchronize(st));
+                if (4 * h > 3 * dn->cpsd_cap) {
+                    int cap = dn->cpsd_cap;
+                    while (4 * h > 3 * cap && cap < 128) cap *= 2;
+                    if ((rc = cpsd_alloc(dn, cap)) != PCD_OK) return rc;
+                }
+            }
+            break;
+        }
         // a radius selection had more members than the list slots: restart from the saved state with twice the slots
         const int cap = dn->cpsd_cap * 2;
-        PCD_CHECK_ARG(attempt < 12 && (int64_t)cap * N < (1ll << 33), "radius selections too large for the device lists");
+        PCD_CHECK_ARG(cap <= 128, "a radius selection holds more than 128 points (the fused CPSD driver's limit; "
+                                  "use the op-by-op path, cpsdDenoise(fused=False))");
         if ((rc = cpsd_alloc(dn, cap)) != PCD_OK) return rc;
         dn->cur = cur0;
         PCD_HIP(hipMemcpyAsync(dn->pos[dn->cur], dn->csave_pos, N * sizeof(float4), hipMemcpyDeviceToDevice, st));

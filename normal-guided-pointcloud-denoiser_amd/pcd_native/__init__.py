@@ -121,6 +121,8 @@ _SIGS = {
     "pcd_host_vu_smooth": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p]),
     "pcd_host_solve3": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "pcd_host_inv3": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "pcd_host_step_csr": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float,
+                                  c_float, c_float, c_void_p]),
     "pcd_host_nvt_tensor": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p]),
 }
 
@@ -744,6 +746,21 @@ def host_inv3(a):
     ok = np.zeros(a.shape[0], np.int32)
     check(lib().pcd_host_inv3(a.ctypes.data, a.shape[0], x.ctypes.data, ok.ctypes.data), "pcd_host_inv3")
     return x, ok.astype(bool)
+
+
+def host_step_csr(kind, pos, n, edge_vectors, ci, nbr, d, alpha, delta=0.0):
+    """The kernels' Denoiser.*_step on the host (dense neighbour rows nbr [m, k]): out [m, 3]."""
+    import numpy as np
+    pos = np.ascontiguousarray(pos, np.float32); n = np.ascontiguousarray(n, np.float32)
+    ev = None if edge_vectors is None else np.ascontiguousarray(edge_vectors, np.float32)
+    ci = np.ascontiguousarray(ci, np.int64); nbr = np.ascontiguousarray(nbr, np.int64)
+    m, k = nbr.shape
+    off = np.arange(m + 1, dtype=np.int64) * k
+    out = np.empty((m, 3), np.float32)
+    check(lib().pcd_host_step_csr(int(kind), pos.ctypes.data, n.ctypes.data, None if ev is None else ev.ctypes.data,
+                                  ci.ctypes.data, off.ctypes.data, nbr.ctypes.data, m, float(delta), float(d),
+                                  float(alpha), out.ctypes.data), "pcd_host_step_csr")
+    return out
 
 
 def orient_normals_mst(pos_host, n_host, a_host, b_host):

@@ -11,5 +11,5 @@ mkdir -p build_$name
   -I../../include -munsafe-fp-atomics $flags -c denoise.hip -o build_$name/denoise.o
 objs=""
 for o in build/*.o; do b=$(basename $o); [ "$b" = denoise.o ] && objs="$objs build_$name/denoise.o" || objs="$objs $o"; done
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../libpcd_$name.so $objs -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../libpcd_$name.so $objs -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
 echo "built libpcd_$name.so ($flags)"
