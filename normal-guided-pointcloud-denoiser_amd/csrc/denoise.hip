@@ -1108,6 +1108,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
     const dim3 grd_rq((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), dense ? 16384 : PCD_RQ_GRID));
     const dim3 grd_wave((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), PCD_REDO_GRID));
+    const dim3 grd_dq((unsigned)std::min<int64_t>(cdiv(rm.nq, 4 * std::max(PCD_DENSE_Q, 1)), 16384));
     const dim3 grd_anc((unsigned)cdiv(rm.nq, kAnchorBS)), grd_cmp((unsigned)cdiv(rm.nq, kCompactBS * kCompactPer));
     int rc = PCD_OK;
     // Dense (no anchors): every row is re-anchored, then NVT1 runs over all rows.  Seeded: the anchor test, then
@@ -1125,8 +1126,12 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     case C:                                                                                                            \
         if (dense) {                                                                                                   \
             if (ev) PCD_HIP(hipEventRecord(ev[1], st));                                                                \
-            hipLaunchKernelGGL((k_knn_requery<2 * C, true>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, PCD_RQ_RDENSE,   \
-                               dn->anc, dn->alist, dn->idx, nullptr, nullptr, dn->spill, spill_cnt);                   \
+            if (PCD_DENSE_Q > 0)                                                                                       \
+                hipLaunchKernelGGL((k_knn_dense_q<2 * C, (PCD_DENSE_Q > 0 ? PCD_DENSE_Q : 1)>), grd_dq, blk, 0, st, gv, P, N, rm, \
+                                   kstore, PCD_RQ_RDENSE, dn->anc, dn->alist, dn->idx, dn->spill, spill_cnt);          \
+            else                                                                                                       \
+                hipLaunchKernelGGL((k_knn_requery<2 * C, true>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, PCD_RQ_RDENSE, \
+                                   dn->anc, dn->alist, dn->idx, nullptr, nullptr, dn->spill, spill_cnt);               \
         } else {                                                                                                       \
             hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd_anc, dim3(kAnchorBS), 0, st, gv, P, N, rm, kstore,        \
                                dn->anc, dn->alist, dn->idx, dn->fail);                                                 \

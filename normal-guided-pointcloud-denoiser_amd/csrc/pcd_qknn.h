@@ -392,9 +392,13 @@ PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo
                     const unsigned long long key2 =
                         ((unsigned long long)__float_as_uint(dist2(q, make_float4(px[u], py[u], pz[u], 0.f))) << 32) | rk[u];
                     const bool pass = j < total && key2 < cap;
+#if defined(PCD_EXP_RQ) && PCD_EXP_RQ == 3    // timing experiment: candidates and distances, no survivors (wrong)
+                    if (pass && key2 == 0ull) buf[0] = key2;
+#else
                     const unsigned long long m = lg.ballot(pass);
                     if (pass) buf[cnt + __popcll(m & ((1ull << hl) - 1ull))] = key2;
                     cnt += __popcll(m);
+#endif
                 }
             }
         }
@@ -413,6 +417,64 @@ struct RqStats { unsigned redo_cnt, spill_cnt, spill_big, spill_amb; };
 #ifndef PCD_RQ_OCC
 #define PCD_RQ_OCC 8
 #endif
+// The end of a re-anchoring query once its survivors are in buf[0..cnt) under cap: the exact order checks, then the
+// stored list, the anchor set (rank order) and the anchor -- or the spill list when a check fails (ok = false on
+// entry: the scan was ambiguous or found too few points).
+template <int KA, int W>
+PCD_DEV void rq_finish(int64_t i, Vec3 q, float r_s, int64_t N, int kstore, float4* __restrict__ anc,
+                       int32_t* __restrict__ alist, int32_t* __restrict__ idx, int32_t* __restrict__ spill,
+                       unsigned* __restrict__ spill_cnt, unsigned long long* buf, int cnt, unsigned long long cap,
+                       bool ok, bool big, const LaneGrp<W>& lg) {
+    const bool partial = cnt < KA;               // (after a buffer cut cnt == KA)
+    GrpOrder<W> o{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, &lg};
+    if (ok) {
+        (void)rq_shrink<KA, W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lg);
+        ok = cnt <= 4 * W;                        // (a set that did not shrink to 4W spills)
+    }
+    if (ok) {
+        o = grp_order32<W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lg);
+        // exact order of the stored list (first kstore + its successor) and of the anchor set boundary
+        ok = order_exact<W>(o, kstore, lg);
+        ok = ok && (cnt <= KA || (o.at(KA) >> 8) != (o.at(KA - 1) >> 8));
+    }
+    if (!ok) {
+        wave_sync();
+        if (lg.hl == 0) {
+            spill[atomicAdd(spill_cnt, 1u)] = (int32_t)i;
+            atomicAdd(big ? spill_cnt + 1 : spill_cnt + 2, 1u);   // RqStats::spill_big / spill_amb
+        }
+        return;
+    }
+    // this lane's elements hl and W + hl of the order; unused slots of a partial set hold N, the snapshot's +inf sentinel row (the anchor test
+    // gives them an infinite distance)
+    const int e0 = lg.hl, e1 = W + lg.hl;
+    const bool h0 = e0 < KA && e0 < cnt, h1 = e1 < KA && e1 < cnt;
+    const unsigned long long m0 = h0 ? buf[o.s0 & 255u] : 0ull;
+    const unsigned long long m1 = h1 ? buf[o.s1 & 255u] : 0ull;
+    const int32_t r0 = h0 ? (int32_t)(uint32_t)(m0 & 0xFFFFFFFFull) : (int32_t)N;   // N: the +inf sentinel row
+    const int32_t r1 = h1 ? (int32_t)(uint32_t)(m1 & 0xFFFFFFFFull) : (int32_t)N;
+    // whole 32-B sectors of the blocked list layout (pcd_lists.h): lanes 8b .. 8b+7 fill block b of row i
+    if (e0 < kstore) idx[lpos(N, i, e0)] = r0;
+    if (e1 < kstore) idx[lpos(N, i, e1)] = r1;
+    // the anchor set is stored in RANK order (unused slots last): the anchor test ranks it by distance itself,
+    // and neighbouring rows -- neighbouring lanes of its waves -- then gather nearly the same snapshot rows in the
+    // same slot, i.e. the same cache lines, instead of 64 unrelated ones per gather instruction
+    {
+        constexpr int M = KA > W ? 2 : 1;
+        uint32_t v[M];
+        v[0] = e0 < KA ? (uint32_t)r0 : 0xFFFFFFFFu;
+        if (M > 1) v[M - 1] = e1 < KA ? (uint32_t)r1 : 0xFFFFFFFFu;
+        grp_bitonic_sort32<W, M>(v, lg.hl);
+        if (e0 < KA) alist[lpos(N, i, e0)] = (int32_t)v[0];
+        if (M > 1 && e1 < KA) alist[lpos(N, i, e1)] = (int32_t)v[M - 1];
+    }
+    // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
+    // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))
+    const unsigned long long mx = grp_max_u64<W>(m0 > m1 ? m0 : m1);
+    const float D = partial ? r_s * (1.f - 1e-6f) : sqrtf(__uint_as_float((unsigned)(mx >> 32)));
+    if (lg.hl == 0) anc[i] = make_float4(q.x, q.y, q.z, D);
+}
+
 // One re-anchoring query (the rows of a lane group; q, i uniform in the group): the exact anchor set within radius
 // r_s (widened x 1.6 up to twice while it holds at most kstore points), the stored list, the new anchor.  Spills an
 // ambiguous or oversized query to the exact-key wave search.  Returns false, having written nothing, when a box
@@ -443,54 +505,7 @@ PCD_DEV bool rq_query(const GridView& g, const Src& src, int64_t i, Vec3 q, floa
         if (ok || !clean) break;
         wave_sync();
     }
-    const bool partial = cnt < KA;               // (after a buffer cut cnt == KA)
-    GrpOrder<W> o{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, &lg};
-    if (ok) {
-        (void)rq_shrink<KA, W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lg);
-        ok = cnt <= 4 * W;                        // (a set that did not shrink to 4W spills)
-    }
-    if (ok) {
-        o = grp_order32<W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lg);
-        // exact order of the stored list (first kstore + its successor) and of the anchor set boundary
-        ok = order_exact<W>(o, kstore, lg);
-        ok = ok && (cnt <= KA || (o.at(KA) >> 8) != (o.at(KA - 1) >> 8));
-    }
-    if (!ok) {
-        wave_sync();
-        if (lg.hl == 0) {
-            spill[atomicAdd(spill_cnt, 1u)] = (int32_t)i;
-            atomicAdd(big ? spill_cnt + 1 : spill_cnt + 2, 1u);   // RqStats::spill_big / spill_amb
-        }
-        return true;
-    }
-    // this lane's elements hl and W + hl of the order; unused slots of a partial set hold N, the snapshot's +inf sentinel row (the anchor test
-    // gives them an infinite distance)
-    const int e0 = lg.hl, e1 = W + lg.hl;
-    const bool h0 = e0 < KA && e0 < cnt, h1 = e1 < KA && e1 < cnt;
-    const unsigned long long m0 = h0 ? buf[o.s0 & 255u] : 0ull;
-    const unsigned long long m1 = h1 ? buf[o.s1 & 255u] : 0ull;
-    const int32_t r0 = h0 ? (int32_t)(uint32_t)(m0 & 0xFFFFFFFFull) : (int32_t)N;   // N: the +inf sentinel row
-    const int32_t r1 = h1 ? (int32_t)(uint32_t)(m1 & 0xFFFFFFFFull) : (int32_t)N;
-    // whole 32-B sectors of the blocked list layout (pcd_lists.h): lanes 8b .. 8b+7 fill block b of row i
-    if (e0 < kstore) idx[lpos(N, i, e0)] = r0;
-    if (e1 < kstore) idx[lpos(N, i, e1)] = r1;
-    // the anchor set is stored in RANK order (unused slots last): the anchor test ranks it by distance itself,
-    // and neighbouring rows -- neighbouring lanes of its waves -- then gather nearly the same snapshot rows in the
-    // same slot, i.e. the same cache lines, instead of 64 unrelated ones per gather instruction
-    {
-        constexpr int M = KA > W ? 2 : 1;
-        uint32_t v[M];
-        v[0] = e0 < KA ? (uint32_t)r0 : 0xFFFFFFFFu;
-        if (M > 1) v[M - 1] = e1 < KA ? (uint32_t)r1 : 0xFFFFFFFFu;
-        grp_bitonic_sort32<W, M>(v, lg.hl);
-        if (e0 < KA) alist[lpos(N, i, e0)] = (int32_t)v[0];
-        if (M > 1 && e1 < KA) alist[lpos(N, i, e1)] = (int32_t)v[M - 1];
-    }
-    // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
-    // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))
-    const unsigned long long mx = grp_max_u64<W>(m0 > m1 ? m0 : m1);
-    const float D = partial ? r_s * (1.f - 1e-6f) : sqrtf(__uint_as_float((unsigned)(mx >> 32)));
-    if (lg.hl == 0) anc[i] = make_float4(q.x, q.y, q.z, D);
+    rq_finish<KA, W>(i, q, r_s, N, kstore, anc, alist, idx, spill, spill_cnt, buf, cnt, cap, ok, big, lg);
     return true;
 }
 
@@ -549,6 +564,195 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
                                           &s_cells[gid], lg);
         (void)done;                                   // (GridSrc covers every box)
         wave_sync();                                  // buf is free for the next query
+    }
+}
+
+// ------------------------------------------------------------------ dense anchoring, Q queries per wave
+// The first iteration re-anchors EVERY row (no anchors yet).  Consecutive rows are spatial neighbours (Morton order),
+// so Q of them share one scan: the union of their boxes is resolved once (cell phase: hash probes, row ranges, the
+// flattened row map) and every candidate row is loaded once, then tested against each query's own cap and appended
+// to that query's survivor buffer.  Each query then finishes exactly as a single one (rq_finish): same survivors under
+// the same cap, same checks, same writes.  A query whose own box is oversized, whose cut was ambiguous, or whose
+// radius holds at most kstore points re-runs alone (rq_query, wider radius) -- the stored lists are exact either way.
+template <int K, int Q, class Src>
+PCD_DEV void rq_scan_box_q(const GridView& g, const Src& src, const Vec3 (&q)[Q], const bool (&act)[Q],
+                           const int lo[3], const int hi[3], unsigned long long (&cap)[Q],
+                           unsigned long long* const (&buf)[Q], int (&cnt)[Q], bool (&clean)[Q], RqCells* wc,
+                           const LaneGrp<64>& lg) {
+    constexpr int W = 64;
+    constexpr int CPL = RqCPL<W>::n;
+    const int hl = lg.hl;
+    const int ex = hi[0] - lo[0] + 1, ey = hi[1] - lo[1] + 1;
+    const int nc = ex * ey * (hi[2] - lo[2] + 1);
+    const uint32_t exy = (uint32_t)ex * (uint32_t)ey;
+    for (int base = 0; base < nc; base += kRqChunk) {
+        int cxs[CPL], cys[CPL], czs[CPL];
+        bool on[CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const uint32_t ci = (uint32_t)(base + hl * CPL + u);
+            on[u] = false; cxs[u] = cys[u] = czs[u] = 0;
+            if (ci < (uint32_t)nc) {
+                const uint32_t zq = ci / exy, rem = ci - zq * exy, yq = rem / (uint32_t)ex;
+                const int cx = lo[0] + (int)(rem - yq * (uint32_t)ex), cy = lo[1] + (int)yq, cz = lo[2] + (int)zq;
+                const float lx = g.ox + cx * g.h, ly = g.oy + cy * g.h, lz = g.oz + cz * g.h;
+#pragma unroll
+                for (int j = 0; j < Q; ++j) {
+                    const float gx = axis_gap(q[j].x, lx, lx + g.h), gy = axis_gap(q[j].y, ly, ly + g.h),
+                                gz = axis_gap(q[j].z, lz, lz + g.h);
+                    const float kth = __uint_as_float((unsigned)(cap[j] >> 32));
+                    on[u] = on[u] || (act[j] && clean[j] && gx * gx + gy * gy + gz * gz <= kth * 1.00001f + 1e-30f);
+                }
+                cxs[u] = cx; cys[u] = cy; czs[u] = cz;
+            }
+        }
+        uint2 cr[CPL];
+        src.template ranges<CPL>(cxs, cys, czs, on, cr);
+        uint32_t loc[CPL], run = 0;
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            run += cr[u].y > cr[u].x ? cr[u].y - cr[u].x : 0u;
+            loc[u] = run;
+        }
+        const uint32_t incl = lane_scan_incl<W>(run);
+        const uint32_t total = lg.bcast(incl, W - 1);
+        if (total == 0) continue;
+        const uint32_t excl = incl - run;
+        wave_sync();
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            wc->start[hl * CPL + u] = cr[u].x;
+            wc->end_incl[hl * CPL + u] = excl + loc[u];
+        }
+        const bool mapped = kRqMap > 0 && total <= (uint32_t)kRqMap;
+        if (mapped) {
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                const uint32_t b = excl + (u ? loc[u - 1] : 0u), e = excl + loc[u];
+                for (uint32_t k = b; k < e; ++k) wc->cellof[k] = (uint8_t)(hl * CPL + u);
+            }
+        }
+        wave_sync();
+        for (uint32_t j0 = 0; j0 < total; j0 += W * kRqRows) {
+#pragma unroll
+            for (int j = 0; j < Q; ++j)
+                if (clean[j] && cnt[j] > RqSurv<W>::n - W * kRqRows && !rq_cut<K, W>(buf[j], cnt[j], cap[j], lg))
+                    clean[j] = false;                 // (this query re-runs alone)
+            uint32_t r[kRqRows];
+#pragma unroll
+            for (int u = 0; u < kRqRows; ++u) {
+                const uint32_t jj = j0 + (uint32_t)(u * W + hl);
+                int a = 0;
+                if (mapped) {
+                    a = jj < total ? (int)wc->cellof[jj] : 0;
+                } else {
+                    int b = kRqChunk - 1;
+#pragma unroll
+                    for (int it = 0; it < kRqChunkLog2; ++it) {
+                        const int m = (a + b) >> 1;
+                        if (wc->end_incl[m] > jj) b = m; else a = m + 1;
+                    }
+                }
+                r[u] = jj < total ? wc->start[a] + (jj - (a ? wc->end_incl[a - 1] : 0u)) : 0u;
+            }
+            float px[kRqRows], py[kRqRows], pz[kRqRows];
+            uint32_t rk[kRqRows];
+#pragma unroll
+            for (int u = 0; u < kRqRows; ++u)
+                if (j0 + (uint32_t)(u * W) < total) src.row(r[u], px[u], py[u], pz[u], rk[u]);
+#pragma unroll
+            for (int u = 0; u < kRqRows; ++u) {
+                const uint32_t jj = j0 + (uint32_t)(u * W + hl);
+                if (j0 + (uint32_t)(u * W) < total) {
+                    const float4 c4 = make_float4(px[u], py[u], pz[u], 0.f);
+#pragma unroll
+                    for (int j = 0; j < Q; ++j) {
+                        const unsigned long long key2 =
+                            ((unsigned long long)__float_as_uint(dist2(q[j], c4)) << 32) | rk[u];
+                        const bool pass = jj < total && act[j] && clean[j] && key2 < cap[j];
+                        const unsigned long long m = lg.ballot(pass);
+                        if (pass) buf[j][cnt[j] + __popcll(m & ((1ull << hl) - 1ull))] = key2;
+                        cnt[j] += __popcll(m);
+                    }
+                }
+            }
+        }
+        wave_sync();
+    }
+}
+
+#ifndef PCD_DENSE_Q
+#define PCD_DENSE_Q 0        // queries per wave of the dense first anchoring (0: one, k_knn_requery<KA, true>)
+#endif
+#ifndef PCD_DQ_OCC
+#define PCD_DQ_OCC 4
+#endif
+template <int KA, int Q>
+__global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, const float4* __restrict__ pos, int64_t N,
+                                                                RowMap rm, int kstore, float r_scale,
+                                                                float4* __restrict__ anc, int32_t* __restrict__ alist,
+                                                                int32_t* __restrict__ idx, int32_t* __restrict__ spill,
+                                                                unsigned* __restrict__ spill_cnt) {
+    constexpr int W = 64;
+    __shared__ unsigned long long s_buf[4][Q][RqSurv<W>::n];
+    __shared__ RqCells s_cells[4];
+    const int lane = (int)(threadIdx.x & 63);
+    const LaneGrp<W> lg(lane);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
+    for (int64_t t0 = (lb * 4 + wv) * Q; t0 < rm.nq; t0 += (int64_t)gridDim.x * 4 * Q) {
+        int64_t iq[Q];
+        Vec3 q[Q];
+        float rs[Q];
+        bool act[Q], clean[Q];
+        unsigned long long cap[Q];
+        int cnt[Q];
+        unsigned long long* bufs[Q];
+        int lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+        bool any_big = false;
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+            act[j] = t0 + j < rm.nq;
+            iq[j] = (int64_t)rfl((uint32_t)rm(act[j] ? t0 + j : t0));
+            const float4 p4 = pos[iq[j]];
+            q[j] = v3(p4.x, p4.y, p4.z);
+            const int cx = min(max(cell_coord(q[j].x, g.ox, g.inv_h), 0), g.dx - 1);
+            const int cy = min(max(cell_coord(q[j].y, g.oy, g.inv_h), 0), g.dy - 1);
+            const int cz = min(max(cell_coord(q[j].z, g.oz, g.inv_h), 0), g.dz - 1);
+            uint32_t s = 0, e = 0;
+            const int n = cell_range(g, cx, cy, cz, s, e) ? (int)(e - s) : 1;
+            rs[j] = r_scale * g.h * cbrtf(16.f / (float)n);
+            cap[j] = ((unsigned long long)__float_as_uint(rs[j] * rs[j]) << 32) | 0xFFFFFFFFull;
+            int l3[3], h3[3];
+            cell_box(g, q[j], rs[j] * 1.0001f + 1e-30f, l3, h3);
+            const int64_t nbox = (int64_t)(h3[0] - l3[0] + 1) * (h3[1] - l3[1] + 1) * (h3[2] - l3[2] + 1);
+            clean[j] = nbox <= kRqMaxCells;           // (an oversized box runs alone and spills there)
+            any_big = any_big || (act[j] && !clean[j]);
+            if (act[j] && clean[j])
+                for (int a = 0; a < 3; ++a) { lo[a] = min(lo[a], l3[a]); hi[a] = max(hi[a], h3[a]); }
+            cnt[j] = 0;
+            bufs[j] = s_buf[wv][j];
+        }
+        const int64_t ubox = lo[0] <= hi[0] ? (int64_t)(hi[0] - lo[0] + 1) * (hi[1] - lo[1] + 1) * (hi[2] - lo[2] + 1) : 0;
+        if (ubox > 0 && ubox <= kRqMaxCells)
+            rq_scan_box_q<KA, Q>(g, GridSrc{&g}, q, act, lo, hi, cap, bufs, cnt, clean, &s_cells[wv], lg);
+        else
+            for (int j = 0; j < Q; ++j) clean[j] = false;   // (the union is too wide: every query alone)
+        (void)any_big;
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+            if (!act[j]) continue;
+            if (clean[j] && cnt[j] > kstore) {
+                rq_finish<KA, W>(iq[j], q[j], rs[j], N, kstore, anc, alist, idx, spill, spill_cnt, bufs[j], cnt[j],
+                                 cap[j], true, false, lg);
+            } else {
+                // alone: its own box (an oversized one spills in there), the radius widened when too few were found
+                wave_sync();
+                (void)rq_query<KA, W>(g, GridSrc{&g}, iq[j], q[j], clean[j] ? rs[j] * 1.6f : rs[j], N, kstore, anc,
+                                      alist, idx, spill, spill_cnt, bufs[j], &s_cells[wv], lg);
+            }
+            wave_sync();
+        }
     }
 }
 
