@@ -59,19 +59,52 @@ __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __res
         const int hi[3] = {min(cell_coord(qx + rf, g.ox, g.inv_h), g.dx - 1),
                            min(cell_coord(qy + rf, g.oy, g.inv_h), g.dy - 1),
                            min(cell_coord(qz + rf, g.oz, g.inv_h), g.dz - 1)};
+        // f32 pre-test: a candidate clearly inside or outside (relative margin 1e-5, far above fp32 rounding of d²)
+        // is decided without the f64 arithmetic; the rest take scipy's exact test
+        const float r2f = (float)r2, r2lo = r2f * (1.f - 1e-5f), r2hi = r2f * (1.f + 1e-5f);
+        unsigned long long last_bkey = ~0ull;
+        uint32_t last_brick = 0u;
+        bool last_ok = false;
         for (int cz = lo[2]; cz <= hi[2]; ++cz)
             for (int cy = lo[1]; cy <= hi[1]; ++cy)
                 for (int cx = lo[0]; cx <= hi[0]; ++cx) {
-                    uint32_t s, e;
-                    if (!cell_range(g, cx, cy, cz, s, e)) continue;
-                    for (uint32_t r0 = s; r0 < e; ++r0) {
-                        const float4 p = g.pts[r0];
-                        const double dx = (double)qx - (double)p.x, dy = (double)qy - (double)p.y,
-                                     dz = (double)qz - (double)p.z;
-                        const double d2 = __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
-                        if (d2 <= r2) {
-                            if (m < CAP) L[m * BS] = ((unsigned long long)__float_as_uint(p.w) << 32) | r0;
-                            ++m;
+                    // the cell's brick (4x4x4 cells) from the hash, reused while the scan stays inside it
+                    const unsigned long long key = morton3(cx, cy, cz), bkey = key >> 6;
+                    if (bkey != last_bkey) {
+                        last_bkey = bkey;
+                        last_ok = false;
+                        unsigned long long slot = hash_slot(bkey, g.hbits);
+                        for (;;) {
+                            const uint4 sl = *reinterpret_cast<const uint4*>(g.table + slot);
+                            const unsigned long long k2 = (unsigned long long)sl.x | ((unsigned long long)sl.y << 32);
+                            if (k2 == bkey) { last_brick = sl.z; last_ok = true; break; }
+                            if (k2 == kEmptyKey) break;
+                            slot = (slot + 1) & g.mask;
+                        }
+                    }
+                    if (!last_ok) continue;
+                    const uint2 ce = g.cells[(uint64_t)last_brick * 64 + (key & 63)];
+                    for (uint32_t r0 = ce.x; r0 < ce.y; r0 += 4) {
+                        float4 p[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) p[u] = g.pts[min(r0 + (uint32_t)u, ce.y - 1u)];   // 4 rows in flight
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            if (r0 + (uint32_t)u >= ce.y) break;
+                            const float fx = qx - p[u].x, fy = qy - p[u].y, fz = qz - p[u].z;
+                            const float d2f = (fx * fx + fy * fy) + fz * fz;
+                            bool in = d2f < r2lo;
+                            if (!in && !(d2f > r2hi)) {
+                                const double dx = (double)qx - (double)p[u].x, dy = (double)qy - (double)p[u].y,
+                                             dz = (double)qz - (double)p[u].z;
+                                const double d2 =
+                                    __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
+                                in = d2 <= r2;
+                            }
+                            if (in) {
+                                if (m < CAP) L[m * BS] = ((unsigned long long)__float_as_uint(p[u].w) << 32) | (r0 + u);
+                                ++m;
+                            }
                         }
                     }
                 }

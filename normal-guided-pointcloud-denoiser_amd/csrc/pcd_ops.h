@@ -141,14 +141,22 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho) {
 // ----------------------------------------------------------------- CPSD: Decompositionor.getNormalFilteredNVT
 // w_ij = acos(clamp(n_i . n_j, -1, 1)) <= rho (no abs, <=; Decompositionor.py:269); T_i = Σ w n_j n_jᵀ / Σ w;
 // a row where no neighbour votes gets n_i n_iᵀ (:273-275).  Sums in list order, like scatter_add.
+// The vote: acos is decreasing, so acos(c) <= rho is c >= cos(rho) -- decided that way when c is more than 1e-6
+// from cos(rho) (acosf's and cosf's roundings are ~1e-7 in c there), else by the reference's own acosf(c) <= rho.
+PCD_DEV bool normal_vote(float c, float rho, float crho) {
+    if (c - crho > 1e-6f) return true;
+    if (crho - c > 1e-6f) return false;
+    return acosf(c) <= rho;
+}
 template <class Nr, class Nb>
 PCD_DEV Sym3 nvt_normal_tensor(Nr nrm, Vec3 ni, int cnt, Nb nb, float rho) {
     float w00 = 0.f, w01 = 0.f, w02 = 0.f, w11 = 0.f, w12 = 0.f, w22 = 0.f;
     int wsum = 0;
+    const float crho = cosf(rho);
     for (int t = 0; t < cnt; ++t) {
         const Vec3 nj = nrm(nb(t));
         const float c = fminf(fmaxf(dot3(ni, nj), -1.f), 1.f);
-        if (acosf(c) <= rho) {
+        if (normal_vote(c, rho, crho)) {
             w00 += nj.x * nj.x; w01 += nj.x * nj.y; w02 += nj.x * nj.z;
             w11 += nj.y * nj.y; w12 += nj.y * nj.z; w22 += nj.z * nj.z;
             ++wsum;
@@ -179,16 +187,17 @@ PCD_DEV Sym3 pvt_normal_cov(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, flo
         return Sym3{a[0], a[1], a[2], a[3], a[4], a[5]};
     }
     int wsum = 0;
+    const float crho = cosf(rho);
     for (int t = 0; t < cnt; ++t) {
         const float c = fminf(fmaxf(dot3(ni, nrm(nb(t))), -1.f), 1.f);
-        wsum += acosf(c) <= rho ? 1 : 0;
+        wsum += normal_vote(c, rho, crho) ? 1 : 0;
     }
     const bool all = wsum == 0;
     if (all) wsum = cnt;
     auto vote = [&](int64_t j) {
         if (all) return true;
         const float c = fminf(fmaxf(dot3(ni, nrm(j)), -1.f), 1.f);
-        return acosf(c) <= rho;
+        return normal_vote(c, rho, crho);
     };
     float sx = 0.f, sy = 0.f, sz = 0.f;
     for (int t = 0; t < cnt; ++t) {
