@@ -252,9 +252,11 @@ struct RqCells {            // per-group LDS scratch for one chunk of cells
 // measured this way: DESIGN §3).
 struct GridSrc {
     const GridView* g;
-    template <int CPL>
+    // OCT (PCD_RQ_OCT builds with an octant index): each cell's range is cut to the rows from the first to the last
+    // octant whose box (widened by the grid's slack) lies within thr (squared) of q
+    template <int CPL, bool OCT = false>
     PCD_DEV void ranges(const int (&cx)[CPL], const int (&cy)[CPL], const int (&cz)[CPL], const bool (&on)[CPL],
-                        uint2 (&cr)[CPL]) const {
+                        uint2 (&cr)[CPL], Vec3 q = Vec3{0.f, 0.f, 0.f}, float thr = 0.f) const {
         uint32_t slot[CPL], loc6[CPL];
         unsigned long long bkey[CPL];
 #pragma unroll
@@ -289,6 +291,36 @@ struct GridSrc {
 #pragma unroll
         for (int u = 0; u < CPL; ++u)
             cr[u] = brick[u] != ~0u ? g->cells[(uint64_t)brick[u] * 64 + loc6[u]] : make_uint2(0u, 0u);
+        if constexpr (OCT && PCD_RQ_OCT) {
+            uint2 oc[CPL];
+#pragma unroll
+            for (int u = 0; u < CPL; ++u)
+                oc[u] = brick[u] != ~0u && g->oct ? g->oct[(uint64_t)brick[u] * 64 + loc6[u]] : make_uint2(0u, 0u);
+            const float hh = 0.5f * g->h, sl = g->slack;
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                if (!(oc[u].x & 1u) || cr[u].y <= cr[u].x) continue;
+                const float lx = g->ox + cx[u] * g->h, ly = g->oy + cy[u] * g->h, lz = g->oz + cz[u] * g->h;
+                float gx[2], gy[2], gz[2];
+                gx[0] = axis_gap(q.x, lx - sl, lx + hh + sl); gx[1] = axis_gap(q.x, lx + hh - sl, lx + g->h + sl);
+                gy[0] = axis_gap(q.y, ly - sl, ly + hh + sl); gy[1] = axis_gap(q.y, ly + hh - sl, ly + g->h + sl);
+                gz[0] = axis_gap(q.z, lz - sl, lz + hh + sl); gz[1] = axis_gap(q.z, lz + hh - sl, lz + g->h + sl);
+                int first = 8, last = -1;
+#pragma unroll
+                for (int o = 0; o < 8; ++o) {
+                    const float a = gx[o & 1], b = gy[(o >> 1) & 1], c = gz[o >> 2];
+                    if (a * a + b * b + c * c <= thr) { first = min(first, o); last = o; }
+                }
+                const uint32_t n = cr[u].y - cr[u].x;
+                auto start = [&](int o) -> uint32_t {
+                    if (o <= 0) return 0u;
+                    if (o >= 8) return n;
+                    return ((o < 4 ? oc[u].x : oc[u].y) >> (8 * (o & 3))) & 0xFFu;
+                };
+                const uint32_t b0 = last < 0 ? 0u : start(first), b1 = last < 0 ? 0u : start(last + 1);
+                cr[u] = make_uint2(cr[u].x + b0, cr[u].x + b1);
+            }
+        }
     }
     PCD_DEV void row(uint32_t r, float& x, float& y, float& z, uint32_t& rank) const {
         const float* pp = reinterpret_cast<const float*>(g->pts + r);
@@ -328,7 +360,7 @@ PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo
             }
         }
         uint2 cr[CPL];
-        src.template ranges<CPL>(cxs, cys, czs, on, cr);
+        src.template ranges<CPL, true>(cxs, cys, czs, on, cr, q, kth * 1.00001f + 1e-30f);
         uint32_t loc[CPL], run = 0;
 #pragma unroll
         for (int u = 0; u < CPL; ++u) {

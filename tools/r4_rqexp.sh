@@ -5,7 +5,8 @@
 set -o pipefail
 export TMPDIR=/tmp
 tag=${1:-r4rq}
-for v in cur rq2 rq3 dq2 dq4; do
+shift; vs=${@:-cur rq2 rq3 dq2 dq4}
+for v in $vs; do
   if [ "$v" = cur ]; then lib=$PWD/normal-guided-pointcloud-denoiser_amd/libpcd.so
   else lib=$PWD/normal-guided-pointcloud-denoiser_amd/libpcd_$v.so; fi
   PCD_LIB=$lib timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$tag/$v -o run -- \
