@@ -13,9 +13,10 @@
 //               (temp_pos = pos.clone()), per-step clamp d * 20000, global clamp ||temp_pos - original_pos|| < d
 //               (the fused loop's jacobi + clamp_global phases, Denoiser.py:26-119)
 //   n := f_n
-// Radius members are collected and sorted in LDS (cap slots a lane, 16 / 32 / 64 / 128) and stored as [N][cap] rows.
-// A row with more than cap members raises a device flag; the call checks it once at the end (its only host sync) and,
-// if set, restores the state it started from, doubles cap and runs again -- results never depend on cap.
+// Radius members are collected and sorted in LDS (cap slots a lane, 16 / 32 / 64 / 128; past 128 in a global
+// slot-major key buffer, the same code) and stored as [N][cap] rows.  A row with more than cap members raises a
+// device flag; the call checks it once at the end (its only host sync) and, if set, restores the state it started
+// from, doubles cap and runs again -- results never depend on cap.
 
 namespace pcd {
 
@@ -23,8 +24,8 @@ static constexpr int kCpsdBS = 128;
 
 // Members of a row's list in ascending original index (the keys' row halves), read from the lane's LDS slots.
 struct LdsKeyNb {
-    const unsigned long long* L;    // this lane's slot 0; slot t at L[t * BS]
-    int bs;
+    const unsigned long long* L;    // this lane's slot 0; slot t at L[t * bs]
+    int64_t bs;
     PCD_DEV int64_t operator()(int t) const { return (int64_t)(uint32_t)(L[t * bs] & 0xFFFFFFFFull); }
 };
 struct RowNb {
@@ -35,19 +36,22 @@ struct RowNb {
 // Radius selection + normal-filtered NVT + VU smoothing of each active row.  The members are collected as
 // (original index << 32 | row) keys in the lane's CAP LDS slots (slot-major: conflict-free), insertion-sorted there
 // (a few dozen LDS round trips, not global ones), summed in that order, and their rows stored for the PVT pass.
+// CAP = 0: the slots are gcap global ones, gk[slot][nq] (selections past the LDS budget; the same code).
 template <int CAP, int BS>
 __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __restrict__ pos,
                                                  const float4* __restrict__ nrm, int64_t N, RowMap rm, float r,
                                                  float rho, float tau, float damp, int32_t* __restrict__ rows,
                                                  int32_t* __restrict__ cnt, float4* __restrict__ fn,
-                                                 int* __restrict__ ovf) {
-    __shared__ unsigned long long s_k[CAP * BS];
+                                                 int* __restrict__ ovf, unsigned long long* __restrict__ gk, int gcap) {
+    __shared__ unsigned long long s_k[CAP > 0 ? CAP * BS : 1];
     const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * BS + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 q4 = pos[i];
     const float qx = q4.x, qy = q4.y, qz = q4.z;
-    unsigned long long* L = s_k + threadIdx.x;
+    const int64_t BSt = CAP > 0 ? (int64_t)BS : rm.nq;     // slot stride
+    const int cap = CAP > 0 ? CAP : gcap;
+    unsigned long long* L = CAP > 0 ? s_k + threadIdx.x : gk + t0;
     int m = 0;
     const double rd = (double)r, r2 = rd * rd;
     if (rd >= 0.0) {
@@ -102,7 +106,7 @@ __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __res
                                 in = d2 <= r2;
                             }
                             if (in) {
-                                if (m < CAP) L[m * BS] = ((unsigned long long)__float_as_uint(p[u].w) << 32) | (r0 + u);
+                                if (m < cap) L[m * BSt] = ((unsigned long long)__float_as_uint(p[u].w) << 32) | (r0 + u);
                                 ++m;
                             }
                         }
@@ -110,26 +114,26 @@ __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __res
                 }
     }
     cnt[i] = m;
-    if (m > CAP) {          // (the call replays with more slots; this row's result is discarded)
+    if (m > cap) {          // (the call replays with more slots; this row's result is discarded)
         atomicOr(ovf, 1);
-        m = CAP;
+        m = cap;
     }
     // ascending original index: scipy's per-query order, the order the reference's scatter sums in
     for (int a = 1; a < m; ++a) {
-        const unsigned long long k = L[a * BS];
+        const unsigned long long k = L[a * BSt];
         int b = a - 1;
         for (; b >= 0; --b) {
-            const unsigned long long kb = L[b * BS];
+            const unsigned long long kb = L[b * BSt];
             if (kb <= k) break;
-            L[(b + 1) * BS] = kb;
+            L[(b + 1) * BSt] = kb;
         }
-        L[(b + 1) * BS] = k;
+        L[(b + 1) * BSt] = k;
     }
-    int32_t* R = rows + (size_t)i * CAP;
-    for (int t = 0; t < m; ++t) R[t] = (int32_t)(uint32_t)(L[t * BS] & 0xFFFFFFFFull);
+    int32_t* R = rows + (size_t)i * cap;
+    for (int t = 0; t < m; ++t) R[t] = (int32_t)(uint32_t)(L[t * BSt] & 0xFFFFFFFFull);
     const float4 n4 = nrm[i];
     const Vec3 ni = v3(n4.x, n4.y, n4.z);
-    const Sym3 T = nvt_normal_tensor(Rows4{nrm}, ni, m, LdsKeyNb{L, BS}, rho);
+    const Sym3 T = nvt_normal_tensor(Rows4{nrm}, ni, m, LdsKeyNb{L, BSt}, rho);
     float w[3], V[3][3];
     eigh3(T, w, V);
     const Vec3 f = vu_smooth(w, V, ni, tau, damp);
@@ -167,10 +171,12 @@ __global__ void k_cpsd_maxcnt(const int32_t* __restrict__ cnt, RowMap rm, int* _
 
 }  // namespace pcd
 
+static constexpr int kCpsdLdsCap = 128;   // larger caps keep their slots in global memory (cgkeys)
+
 static void destroy_cpsd_state(pcd_denoiser* dn) {
     (void)hipFree(dn->ckeys); (void)hipFree(dn->ccnt); (void)hipFree(dn->covf);
-    (void)hipFree(dn->csave_pos); (void)hipFree(dn->csave_nrm);
-    dn->ckeys = nullptr; dn->ccnt = nullptr; dn->covf = nullptr;
+    (void)hipFree(dn->csave_pos); (void)hipFree(dn->csave_nrm); (void)hipFree(dn->cgkeys);
+    dn->ckeys = nullptr; dn->ccnt = nullptr; dn->covf = nullptr; dn->cgkeys = nullptr;
     dn->csave_pos = dn->csave_nrm = nullptr;
     dn->cpsd_cap = 0;
 }
@@ -178,10 +184,14 @@ static void destroy_cpsd_state(pcd_denoiser* dn) {
 static int cpsd_alloc(pcd_denoiser* dn, int cap) {
     const int64_t N = dn->n;
     (void)hipFree(dn->ckeys);
+    (void)hipFree(dn->cgkeys);
     dn->ckeys = nullptr;
+    dn->cgkeys = nullptr;
     dn->cpsd_cap = 0;
     if (hipMalloc(&dn->ckeys, (size_t)N * (size_t)cap * sizeof(int32_t)) != hipSuccess)
         return fail(PCD_ERR_OOM, "pcd_cpsd_iterate: radius lists");
+    if (cap > kCpsdLdsCap && hipMalloc(&dn->cgkeys, (size_t)N * (size_t)cap * sizeof(unsigned long long)) != hipSuccess)
+        return fail(PCD_ERR_OOM, "pcd_cpsd_iterate: radius list slots");
     if (!dn->ccnt && (hipMalloc(&dn->ccnt, N * sizeof(int32_t)) != hipSuccess ||
                       hipMalloc(&dn->covf, sizeof(int)) != hipSuccess ||
                       hipMalloc(&dn->csave_pos, N * sizeof(float4)) != hipSuccess ||
@@ -233,11 +243,12 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
                 const int cap = dn->cpsd_cap;
 #define PCD_CPSD_NVT(C, B)                                                                                             \
     hipLaunchKernelGGL((k_cpsd_nvt<C, B>), dim3((unsigned)cdiv(rm.nq, B)), dim3(B), 0, st, gv, dn->pos[dn->cur], dn->nrm, \
-                       N, rm, cp->r, cp->rho, cp->tau, cp->damp, dn->ckeys, dn->ccnt, dn->fn, dn->covf)
+                       N, rm, cp->r, cp->rho, cp->tau, cp->damp, dn->ckeys, dn->ccnt, dn->fn, dn->covf, dn->cgkeys, cap)
                 if (cap == 16) PCD_CPSD_NVT(16, 128);
                 else if (cap == 32) PCD_CPSD_NVT(32, 128);
                 else if (cap == 64) PCD_CPSD_NVT(64, 64);
-                else PCD_CPSD_NVT(128, 64);
+                else if (cap == 128) PCD_CPSD_NVT(128, 64);
+                else PCD_CPSD_NVT(0, 128);
 #undef PCD_CPSD_NVT
                 hipLaunchKernelGGL(k_cpsd_pvt, grd, blk, 0, st, dn->pos[dn->cur], dn->fn, N, rm, cp->rho, cp->tau,
                                    dn->ckeys, cap, dn->ccnt, dn->cls, dn->edge);
@@ -262,7 +273,7 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
         if (!ovf || iterations == 0) {
             // slots for the next call with headroom: the largest selection of the last iteration above 3/4 of the
             // slots doubles them now, so a later call does not replay when the points drift into denser spots
-            if (iterations > 0 && dn->cpsd_cap < 128 && rm.nq > 0) {
+            if (iterations > 0 && rm.nq > 0) {
                 int* mx = dn->covf;                       // (reused as the max-count cell)
                 PCD_HIP(hipMemsetAsync(mx, 0, sizeof(int), st));
                 hipLaunchKernelGGL(k_cpsd_maxcnt, dim3((unsigned)std::min<int64_t>(cdiv(rm.nq, 256), 1024)), dim3(256),
@@ -272,7 +283,7 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
                 PCD_HIP(hipStreamSynchronize(st));
                 if (4 * h > 3 * dn->cpsd_cap) {
                     int cap = dn->cpsd_cap;
-                    while (4 * h > 3 * cap && cap < 128) cap *= 2;
+                    while (4 * h > 3 * cap) cap *= 2;
                     if ((rc = cpsd_alloc(dn, cap)) != PCD_OK) return rc;
                 }
             }
@@ -280,8 +291,7 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
         }
         // a radius selection had more members than the list slots: restart from the saved state with twice the slots
         const int cap = dn->cpsd_cap * 2;
-        PCD_CHECK_ARG(cap <= 128, "a radius selection holds more than 128 points (the fused CPSD driver's limit; "
-                                  "use the op-by-op path, cpsdDenoise(fused=False))");
+        PCD_CHECK_ARG(cap <= (1 << 20), "a radius selection holds more than 2^20 points");
         if ((rc = cpsd_alloc(dn, cap)) != PCD_OK) return rc;
         dn->cur = cur0;
         PCD_HIP(hipMemcpyAsync(dn->pos[dn->cur], dn->csave_pos, N * sizeof(float4), hipMemcpyDeviceToDevice, st));

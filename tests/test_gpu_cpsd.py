@@ -165,13 +165,14 @@ def test_cpsd_driver_matches_reference(cpsd, gpu):
         moved = np.linalg.norm(v.cpu().numpy() - pos0, axis=1)
         assert moved.max() < d                                        # the global clamp (ipynb:1060-1061)
 
-@pytest.mark.parametrize("rscale", [1.0, 2.5], ids=["r_d", "r_2.5d_slot_growth"])
+@pytest.mark.parametrize("rscale", [1.0, 1.8, 2.5], ids=["r_d", "r_1.8d_lds_slots", "r_2.5d_global_slots"])
 def test_cpsd_fused_equals_op_by_op(cpsd, gpu, rscale):
     """pcd_cpsd_iterate (the whole loop in one call: radius members sorted in LDS, the fused loop's Jacobi phases with
     the global clamp) against the same operators run op by op through the drop-in classes (cpsdDenoise(fused=False)):
     2 iterations within 1e-6 x bbox (the flat step's global centre is reduced in two different orders).  At
-    r = 2.5 d the selections hold ~80 points: the call starts with 16 list slots, overflows, and replays from its
-    saved state with more -- the result must not depend on it."""
+    r = 1.8 d the selections hold ~50 points (at most ~90): the call starts with 16 list slots, overflows, and
+    replays from its saved state with more LDS slots; at r = 2.5 d (~100, at most ~190) it grows past the 128 LDS
+    slots into global ones -- the result must not depend on either."""
     pos0, n0 = cpsd["pos"], cpsd["n"]
     d = float(cpsd["drv_d"])
     bbox = float(np.linalg.norm(pos0.max(0) - pos0.min(0)))

@@ -5,6 +5,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 tag=${1:-r4rq}
+mkdir -p gpurun_out/$tag
 shift; vs=${@:-cur rq2 rq3 dq2 dq4}
 for v in $vs; do
   if [ "$v" = cur ]; then lib=$PWD/normal-guided-pointcloud-denoiser_amd/libpcd.so
