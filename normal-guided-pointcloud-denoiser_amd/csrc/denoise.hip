@@ -1070,11 +1070,14 @@ static int select_rows(pcd_denoiser* dn, const RowMap& rm, int32_t* list, unsign
 // Anchored K1 (seeded, list cap K <= 32, KA = 2K): the anchor test for every active row, then the re-anchoring
 // search (pcd_qknn.h) of the rows that failed it -- or of every row when there are no anchors (of this KA) yet --
 // and the exact-key wave search (pcd_wknn.h) for the few rows it spills.
+#ifndef PCD_RQ_WD
+#define PCD_RQ_WD PCD_RQ_W     // lanes per query of the one-query dense launch (PCD_DENSE_Q = 0)
+#endif
 #ifndef PCD_RQ_RDENSE
 #define PCD_RQ_RDENSE 1.1f   // first iteration at 10M: 1.45 35.3 ms, 1.3 31.7, 1.2 29.7 (16-point cells); 1.2 26.0-26.7, 1.1 24.3 (32-point cells)
 #endif
 #ifndef PCD_RQ_GRID
-#define PCD_RQ_GRID 4096
+#define PCD_RQ_GRID 8192     // steady re-anchoring blocks (A/B at 10M: 4096 / 8192 / 16384 -> requery 1.23 / 1.18 / 1.17 ms)
 #endif
 #ifndef PCD_REDO_COMPACT
 #define PCD_REDO_COMPACT 1   // the redo list by k_compact_fail (one atomic per 4,096 rows); 0: rocprim::select (row order)
@@ -1131,7 +1134,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
                 hipLaunchKernelGGL((k_knn_dense_q<2 * C, (PCD_DENSE_Q > 0 ? PCD_DENSE_Q : 1)>), grd_dq, blk, 0, st, gv, P, N, rm, \
                                    kstore, PCD_RQ_RDENSE, dn->anc, dn->alist, dn->idx, dn->spill, spill_cnt);          \
             else                                                                                                       \
-                hipLaunchKernelGGL((k_knn_requery<2 * C, true>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, PCD_RQ_RDENSE, \
+                hipLaunchKernelGGL((k_knn_requery<2 * C, true, PCD_RQ_WD>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, PCD_RQ_RDENSE, \
                                    dn->anc, dn->alist, dn->idx, nullptr, nullptr, dn->spill, spill_cnt);               \
         } else {                                                                                                       \
             hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd_anc, dim3(kAnchorBS), 0, st, gv, P, N, rm, kstore,        \

@@ -246,6 +246,23 @@ struct RqCells {            // per-group LDS scratch for one chunk of cells
     uint32_t end_incl[kRqChunk];
     uint8_t cellof[kRqMap > 0 ? kRqMap : 4];   // cell (slot in the chunk) of each flattened candidate row
 };
+// cellof[b..e) = v: the bytes up to the first 4-byte boundary and after the last one singly (a neighbouring lane's run
+// may share those words), the whole words between as one 32-bit store each -- a quarter of the per-byte loop's trips
+// (PCD_RQ_FILL32 = 0: the per-byte loop)
+#ifndef PCD_RQ_FILL32
+#define PCD_RQ_FILL32 0      // 1: A/B at 10M, dense first anchoring 22.1 vs 21.8 ms, steady requery equal: the byte loop kept
+#endif
+PCD_DEV void fill_cellof(uint8_t* cellof, uint32_t b, uint32_t e, uint32_t v) {
+    if (PCD_RQ_FILL32) {
+        const uint32_t wb = min((b + 3u) & ~3u, e), we = max(e & ~3u, wb);
+        for (uint32_t k = b; k < wb; ++k) cellof[k] = (uint8_t)v;
+        const uint32_t v4 = v * 0x01010101u;
+        for (uint32_t k = wb; k < we; k += 4) *reinterpret_cast<uint32_t*>(cellof + k) = v4;
+        for (uint32_t k = we; k < e; ++k) cellof[k] = (uint8_t)v;
+    } else {
+        for (uint32_t k = b; k < e; ++k) cellof[k] = (uint8_t)v;
+    }
+}
 // Where a scan reads its cells and candidate rows from: GridSrc is the grid in global memory (brick hash probes,
 // brick cell blocks, snapshot rows; a row's rank is its index).  A source only has to resolve a lane's cells to row
 // ranges, load a row with its rank, and say whether it covers a cell box (an LDS-staged brick neighbourhood was
@@ -382,13 +399,11 @@ PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo
         const bool mapped = kRqMap > 0 && total <= (uint32_t)kRqMap;   // (group-uniform)
         if (mapped) {
 #pragma unroll
-            for (int u = 0; u < CPL; ++u) {
-                const uint32_t b = excl + (u ? loc[u - 1] : 0u), e = excl + loc[u];
-                for (uint32_t k = b; k < e; ++k) wc->cellof[k] = (uint8_t)(hl * CPL + u);
-            }
+            for (int u = 0; u < CPL; ++u)
+                fill_cellof(wc->cellof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], (uint32_t)(hl * CPL + u));
         }
         wave_sync();
-#if defined(PCD_EXP_RQ) && PCD_EXP_RQ == 2    // timing experiment: cell phase only (results wrong)
+#if defined(PCD_EXP_RQ) && (PCD_EXP_RQ == 2 || PCD_EXP_RQ == 4)    // timing experiment: cell phase only (results wrong)
         if (total != 0x7FFFFFFF) { wave_sync(); continue; }
 #endif
         for (uint32_t j0 = 0; j0 < total; j0 += W * kRqRows) {
@@ -533,6 +548,13 @@ PCD_DEV bool rq_query(const GridView& g, const Src& src, int64_t i, Vec3 q, floa
         if (big) break;
         if (!src.covers(lo, hi)) return false;    // (block-uniform per query: every lane of the group)
         const bool clean = rq_scan_box<KA, W>(g, src, q, lo, hi, cap, buf, cnt, wc, lg);
+#if defined(PCD_EXP_RQ) && PCD_EXP_RQ >= 4      // timing experiment: no finish, no widening (every row spills)
+        if (cnt != -12345) {            // a valid (wrong) list: the row itself; the anchor stays unset
+            if (lg.hl < kstore) idx[lpos(N, i, lg.hl)] = (int32_t)i;
+            if (W + lg.hl < kstore) idx[lpos(N, i, W + lg.hl)] = (int32_t)i;
+            return true;
+        }
+#endif
         ok = clean && cnt > kstore;
         if (ok || !clean) break;
         wave_sync();
@@ -659,10 +681,8 @@ PCD_DEV void rq_scan_box_q(const GridView& g, const Src& src, const Vec3 (&q)[Q]
         const bool mapped = kRqMap > 0 && total <= (uint32_t)kRqMap;
         if (mapped) {
 #pragma unroll
-            for (int u = 0; u < CPL; ++u) {
-                const uint32_t b = excl + (u ? loc[u - 1] : 0u), e = excl + loc[u];
-                for (uint32_t k = b; k < e; ++k) wc->cellof[k] = (uint8_t)(hl * CPL + u);
-            }
+            for (int u = 0; u < CPL; ++u)
+                fill_cellof(wc->cellof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], (uint32_t)(hl * CPL + u));
         }
         wave_sync();
         for (uint32_t j0 = 0; j0 < total; j0 += W * kRqRows) {
