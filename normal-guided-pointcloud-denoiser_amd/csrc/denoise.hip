@@ -996,7 +996,7 @@ struct pcd_denoiser {
     XField xfield{};
     // CPSD driver (pcd_cpsd.h): radius member rows, member counts, overflow flag
     bool nvt1_on = true;          // K1 runs NVT1 after the kNN (off: the lists only)
-    int32_t* ckeys = nullptr;                            // [N][cpsd_cap] member rows, ascending original index
+    int32_t* ckeys = nullptr;                            // [cpsd_cap][nq] member rows (slot-major), ascending original index
     int32_t* ccnt = nullptr;
     unsigned long long* cgkeys = nullptr;                // [cpsd_cap][nq] member keys when cpsd_cap > 128 (else LDS)
     int* covf = nullptr;

@@ -14,7 +14,8 @@
 //               (the fused loop's jacobi + clamp_global phases, Denoiser.py:26-119)
 //   n := f_n
 // Radius members are collected and sorted in LDS (cap slots a lane, 16 / 32 / 64 / 128; past 128 in a global
-// slot-major key buffer, the same code) and stored as [N][cap] rows.  A row with more than cap members raises a
+// slot-major key buffer, the same code) and stored slot-major, [cap][nq] rows (a wave's lanes read one slot
+// together: whole lines).  A row with more than cap members raises a
 // device flag; the call checks it once at the end (its only host sync) and, if set, restores the state it started
 // from, doubles cap and runs again -- results never depend on cap.
 
@@ -28,9 +29,10 @@ struct LdsKeyNb {
     int64_t bs;
     PCD_DEV int64_t operator()(int t) const { return (int64_t)(uint32_t)(L[t * bs] & 0xFFFFFFFFull); }
 };
-struct RowNb {
+struct RowNb {              // slot-major member rows: slot t at L[t * stride]
     const int32_t* L;
-    PCD_DEV int64_t operator()(int t) const { return L[t]; }
+    int64_t stride;
+    PCD_DEV int64_t operator()(int t) const { return L[t * stride]; }
 };
 
 // Radius selection + normal-filtered NVT + VU smoothing of each active row.  The members are collected as
@@ -129,8 +131,8 @@ __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __res
         }
         L[(b + 1) * BSt] = k;
     }
-    int32_t* R = rows + (size_t)i * cap;
-    for (int t = 0; t < m; ++t) R[t] = (int32_t)(uint32_t)(L[t * BSt] & 0xFFFFFFFFull);
+    int32_t* R = rows + t0;
+    for (int t = 0; t < m; ++t) R[t * rm.nq] = (int32_t)(uint32_t)(L[t * BSt] & 0xFFFFFFFFull);
     const float4 n4 = nrm[i];
     const Vec3 ni = v3(n4.x, n4.y, n4.z);
     const Sym3 T = nvt_normal_tensor(Rows4{nrm}, ni, m, LdsKeyNb{L, BSt}, rho);
@@ -152,7 +154,7 @@ __global__ __launch_bounds__(kCpsdBS) void k_cpsd_pvt(const float4* __restrict__
     const int m = min(cnt[i], cap);
     const float4 p4 = pos[i], f4 = fn[i];
     const Sym3 C = pvt_normal_cov(Rows4{pos}, Rows4{fn}, v3(p4.x, p4.y, p4.z), v3(f4.x, f4.y, f4.z), m,
-                                  RowNb{rows + (size_t)i * cap}, rho);
+                                  RowNb{rows + t0, rm.nq}, rho);
     float w[3], V[3][3];
     eigh3(C, w, V);
     // getVUFeatures(tau) = (eigval < tau).sum(dim=1) % 3 (Decompositionor.py:84-85); NaN compares false
@@ -171,7 +173,10 @@ __global__ void k_cpsd_maxcnt(const int32_t* __restrict__ cnt, RowMap rm, int* _
 
 }  // namespace pcd
 
-static constexpr int kCpsdLdsCap = 128;   // larger caps keep their slots in global memory (cgkeys)
+#ifndef PCD_CPSD_LDS_MAX
+#define PCD_CPSD_LDS_MAX 128
+#endif
+static constexpr int kCpsdLdsCap = PCD_CPSD_LDS_MAX;   // larger caps keep their slots in global memory (cgkeys)
 
 static void destroy_cpsd_state(pcd_denoiser* dn) {
     (void)hipFree(dn->ckeys); (void)hipFree(dn->ccnt); (void)hipFree(dn->covf);
@@ -244,11 +249,14 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
 #define PCD_CPSD_NVT(C, B)                                                                                             \
     hipLaunchKernelGGL((k_cpsd_nvt<C, B>), dim3((unsigned)cdiv(rm.nq, B)), dim3(B), 0, st, gv, dn->pos[dn->cur], dn->nrm, \
                        N, rm, cp->r, cp->rho, cp->tau, cp->damp, dn->ckeys, dn->ccnt, dn->fn, dn->covf, dn->cgkeys, cap)
-                if (cap == 16) PCD_CPSD_NVT(16, 128);
+                // LDS slots cost occupancy (cap x 8 B a lane): past 16 slots they pay only on a launch too small to
+                // fill the chip anyway (A/B: 50k points 0.23 LDS vs 0.29 ms global; 1M at 64 slots 1.79 vs 1.42 ms)
+                const bool lds = cap <= 16 || (cap <= kCpsdLdsCap && rm.nq <= (int64_t)1 << 18);
+                if (!lds) PCD_CPSD_NVT(0, 128);
+                else if (cap == 16) PCD_CPSD_NVT(16, 128);
                 else if (cap == 32) PCD_CPSD_NVT(32, 128);
                 else if (cap == 64) PCD_CPSD_NVT(64, 64);
-                else if (cap == 128) PCD_CPSD_NVT(128, 64);
-                else PCD_CPSD_NVT(0, 128);
+                else PCD_CPSD_NVT(128, 64);
 #undef PCD_CPSD_NVT
                 hipLaunchKernelGGL(k_cpsd_pvt, grd, blk, 0, st, dn->pos[dn->cur], dn->fn, N, rm, cp->rho, cp->tau,
                                    dn->ckeys, cap, dn->ccnt, dn->cls, dn->edge);
