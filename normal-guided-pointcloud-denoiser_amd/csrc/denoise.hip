@@ -998,7 +998,7 @@ struct pcd_denoiser {
     bool nvt1_on = true;          // K1 runs NVT1 after the kNN (off: the lists only)
     int32_t* ckeys = nullptr;                            // [cpsd_cap][nq] member rows (slot-major), ascending original index
     int32_t* ccnt = nullptr;
-    unsigned long long* cgkeys = nullptr;                // [cpsd_cap][nq] member keys when cpsd_cap > 128 (else LDS)
+    int32_t* cinv = nullptr;                             // original index -> snapshot row (the grid's perm inverted)
     int* covf = nullptr;
     int cpsd_cap = 0;
     float4 *csave_pos = nullptr, *csave_nrm = nullptr;   // the state at the call's start (a replay after overflow)

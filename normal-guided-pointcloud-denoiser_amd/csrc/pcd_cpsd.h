@@ -13,47 +13,58 @@
 //               (temp_pos = pos.clone()), per-step clamp d * 20000, global clamp ||temp_pos - original_pos|| < d
 //               (the fused loop's jacobi + clamp_global phases, Denoiser.py:26-119)
 //   n := f_n
-// Radius members are collected and sorted in LDS (cap slots a lane, 16 / 32 / 64 / 128; past 128 in a global
-// slot-major key buffer, the same code) and stored slot-major, [cap][nq] rows (a wave's lanes read one slot
-// together: whole lines).  A row with more than cap members raises a
-// device flag; the call checks it once at the end (its only host sync) and, if set, restores the state it started
-// from, doubles cap and runs again -- results never depend on cap.
+// Radius members are collected as their ORIGINAL indices (the sort key) -- the first 32 in the lane's LDS slots, any
+// further ones in the row's own slots of the member-row buffer -- insertion-sorted there, and mapped back to snapshot
+// rows through the inverse permutation; the rows are stored slot-major, [cap][nq] (a wave's lanes read one slot
+// together: whole lines).  A row with more than cap members raises a device flag; the call checks it once at the end
+// (its only host sync) and, if set, restores the state it started from, doubles cap and runs again -- results never
+// depend on cap.
 
 namespace pcd {
 
 static constexpr int kCpsdBS = 128;
+#ifndef PCD_CPSD_CELLS
+#define PCD_CPSD_CELLS 4
+#endif
+static constexpr int kCpsdCells = PCD_CPSD_CELLS;   // box cells looked up together by a lane
 
-// Members of a row's list in ascending original index (the keys' row halves), read from the lane's LDS slots.
-struct LdsKeyNb {
-    const unsigned long long* L;    // this lane's slot 0; slot t at L[t * bs]
-    int64_t bs;
-    PCD_DEV int64_t operator()(int t) const { return (int64_t)(uint32_t)(L[t * bs] & 0xFFFFFFFFull); }
-};
 struct RowNb {              // slot-major member rows: slot t at L[t * stride]
     const int32_t* L;
     int64_t stride;
     PCD_DEV int64_t operator()(int t) const { return L[t * stride]; }
 };
 
-// Radius selection + normal-filtered NVT + VU smoothing of each active row.  The members are collected as
-// (original index << 32 | row) keys in the lane's CAP LDS slots (slot-major: conflict-free), insertion-sorted there
-// (a few dozen LDS round trips, not global ones), summed in that order, and their rows stored for the PVT pass.
-// CAP = 0: the slots are gcap global ones, gk[slot][nq] (selections past the LDS budget; the same code).
-template <int CAP, int BS>
+// A lane's member slots: slot t < L in LDS (slot-major across the block: conflict-free), past that the row's own
+// slots of the member-row buffer (rows[t][nq], the row's column t0).
+template <int L>
+struct CpsdSlots {
+    uint32_t* lds;              // this lane's slot 0; slot t at lds[t * BS]
+    int bs;
+    uint32_t* glb;              // rows + t0; slot t at glb[t * nq]
+    int64_t nq;
+    PCD_DEV uint32_t get(int t) const { return t < L ? lds[t * bs] : glb[t * nq]; }
+    PCD_DEV void set(int t, uint32_t v) const {
+        if (t < L) lds[t * bs] = v; else glb[t * nq] = v;
+    }
+};
+
+// Radius selection + normal-filtered NVT + VU smoothing of each active row.  Members are collected as their original
+// indices (scipy's order key) in the lane's slots, insertion-sorted there, mapped to snapshot rows through inv
+// (original index -> row), stored slot-major for the PVT pass and summed in that order.  CAP: the call's slots (L of
+// them in LDS: 32 x 4 B a lane keeps 5 waves/SIMD).
+template <int L, int BS>
 __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __restrict__ pos,
                                                  const float4* __restrict__ nrm, int64_t N, RowMap rm, float r,
                                                  float rho, float tau, float damp, int32_t* __restrict__ rows,
                                                  int32_t* __restrict__ cnt, float4* __restrict__ fn,
-                                                 int* __restrict__ ovf, unsigned long long* __restrict__ gk, int gcap) {
-    __shared__ unsigned long long s_k[CAP > 0 ? CAP * BS : 1];
+                                                 int* __restrict__ ovf, const int32_t* __restrict__ inv, int cap) {
+    __shared__ uint32_t s_k[L * BS];
     const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * BS + threadIdx.x;
     if (t0 >= rm.nq) return;
     const int64_t i = rm(t0);
     const float4 q4 = pos[i];
     const float qx = q4.x, qy = q4.y, qz = q4.z;
-    const int64_t BSt = CAP > 0 ? (int64_t)BS : rm.nq;     // slot stride
-    const int cap = CAP > 0 ? CAP : gcap;
-    unsigned long long* L = CAP > 0 ? s_k + threadIdx.x : gk + t0;
+    const CpsdSlots<L> S{s_k + threadIdx.x, BS, reinterpret_cast<uint32_t*>(rows) + t0, rm.nq};
     int m = 0;
     const double rd = (double)r, r2 = rd * rd;
     if (rd >= 0.0) {
@@ -68,52 +79,90 @@ __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __res
         // f32 pre-test: a candidate clearly inside or outside (relative margin 1e-5, far above fp32 rounding of d²)
         // is decided without the f64 arithmetic; the rest take scipy's exact test
         const float r2f = (float)r2, r2lo = r2f * (1.f - 1e-5f), r2hi = r2f * (1.f + 1e-5f);
-        unsigned long long last_bkey = ~0ull;
-        uint32_t last_brick = 0u;
-        bool last_ok = false;
-        for (int cz = lo[2]; cz <= hi[2]; ++cz)
-            for (int cy = lo[1]; cy <= hi[1]; ++cy)
-                for (int cx = lo[0]; cx <= hi[0]; ++cx) {
-                    // the cell's brick (4x4x4 cells) from the hash, reused while the scan stays inside it
-                    const unsigned long long key = morton3(cx, cy, cz), bkey = key >> 6;
-                    if (bkey != last_bkey) {
-                        last_bkey = bkey;
-                        last_ok = false;
-                        unsigned long long slot = hash_slot(bkey, g.hbits);
-                        for (;;) {
-                            const uint4 sl = *reinterpret_cast<const uint4*>(g.table + slot);
-                            const unsigned long long k2 = (unsigned long long)sl.x | ((unsigned long long)sl.y << 32);
-                            if (k2 == bkey) { last_brick = sl.z; last_ok = true; break; }
-                            if (k2 == kEmptyKey) break;
-                            slot = (slot + 1) & g.mask;
-                        }
+        // the box's cells in chunks of kCpsdCells, every lookup of a chunk in flight together: cells whose box
+        // (widened by the grid's key slack) lies beyond r are skipped, then the chunk's brick probes, then its row
+        // ranges, then its rows (4 in flight)
+        const float h = g.h, sl = g.slack, r2c = r2f * (1.f + 1e-5f) + 1e-30f;
+        int cx = lo[0], cy = lo[1], cz = lo[2];
+        bool more = lo[0] <= hi[0] && lo[1] <= hi[1] && lo[2] <= hi[2];
+        while (more) {
+            int ccx[kCpsdCells], ccy[kCpsdCells], ccz[kCpsdCells];
+            bool on[kCpsdCells];
+#pragma unroll
+            for (int u = 0; u < kCpsdCells; ++u) {
+                on[u] = more;
+                ccx[u] = cx; ccy[u] = cy; ccz[u] = cz;
+                if (more && ++cx > hi[0]) {
+                    cx = lo[0];
+                    if (++cy > hi[1]) { cy = lo[1]; if (++cz > hi[2]) more = false; }
+                }
+                if (on[u]) {
+                    const float lx = g.ox + ccx[u] * h, ly = g.oy + ccy[u] * h, lz = g.oz + ccz[u] * h;
+                    const float gx = axis_gap(qx, lx - sl, lx + h + sl), gy = axis_gap(qy, ly - sl, ly + h + sl),
+                                gz = axis_gap(qz, lz - sl, lz + h + sl);
+                    on[u] = gx * gx + gy * gy + gz * gz <= r2c;
+                }
+            }
+            unsigned long long bkey[kCpsdCells];
+            uint32_t sidx[kCpsdCells], loc6[kCpsdCells];
+            uint4 e[kCpsdCells];
+#pragma unroll
+            for (int u = 0; u < kCpsdCells; ++u) {
+                bkey[u] = kEmptyKey; sidx[u] = 0; loc6[u] = 0;
+                if (on[u]) {
+                    const unsigned long long key = morton3(ccx[u], ccy[u], ccz[u]);
+                    bkey[u] = key >> 6;
+                    loc6[u] = (uint32_t)(key & 63);
+                    sidx[u] = (uint32_t)hash_slot(bkey[u], g.hbits);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kCpsdCells; ++u)
+                e[u] = on[u] ? *reinterpret_cast<const uint4*>(g.table + sidx[u]) : make_uint4(~0u, ~0u, 0u, 0u);
+            uint2 cr[kCpsdCells];
+#pragma unroll
+            for (int u = 0; u < kCpsdCells; ++u) {
+                uint32_t brick = ~0u;
+                if (on[u]) {
+                    for (;;) {
+                        const unsigned long long k2 = (unsigned long long)e[u].x | ((unsigned long long)e[u].y << 32);
+                        if (k2 == bkey[u]) { brick = e[u].z; break; }
+                        if (k2 == kEmptyKey) break;
+                        sidx[u] = (uint32_t)((sidx[u] + 1) & g.mask);
+                        e[u] = *reinterpret_cast<const uint4*>(g.table + sidx[u]);
                     }
-                    if (!last_ok) continue;
-                    const uint2 ce = g.cells[(uint64_t)last_brick * 64 + (key & 63)];
-                    for (uint32_t r0 = ce.x; r0 < ce.y; r0 += 4) {
-                        float4 p[4];
+                }
+                cr[u] = make_uint2(0u, 0u);
+                if (brick != ~0u) cr[u] = g.cells[(uint64_t)brick * 64 + loc6[u]];
+            }
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) p[u] = g.pts[min(r0 + (uint32_t)u, ce.y - 1u)];   // 4 rows in flight
+            for (int u = 0; u < kCpsdCells; ++u) {
+                const uint2 ce = cr[u];
+                for (uint32_t r0 = ce.x; r0 < ce.y; r0 += 4) {
+                    float4 p[4];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            if (r0 + (uint32_t)u >= ce.y) break;
-                            const float fx = qx - p[u].x, fy = qy - p[u].y, fz = qz - p[u].z;
-                            const float d2f = (fx * fx + fy * fy) + fz * fz;
-                            bool in = d2f < r2lo;
-                            if (!in && !(d2f > r2hi)) {
-                                const double dx = (double)qx - (double)p[u].x, dy = (double)qy - (double)p[u].y,
-                                             dz = (double)qz - (double)p[u].z;
-                                const double d2 =
-                                    __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
-                                in = d2 <= r2;
-                            }
-                            if (in) {
-                                if (m < cap) L[m * BSt] = ((unsigned long long)__float_as_uint(p[u].w) << 32) | (r0 + u);
-                                ++m;
-                            }
+                    for (int w = 0; w < 4; ++w) p[w] = g.pts[min(r0 + (uint32_t)w, ce.y - 1u)];   // 4 rows in flight
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        if (r0 + (uint32_t)w >= ce.y) break;
+                        const float fx = qx - p[w].x, fy = qy - p[w].y, fz = qz - p[w].z;
+                        const float d2f = (fx * fx + fy * fy) + fz * fz;
+                        bool in = d2f < r2lo;
+                        if (!in && !(d2f > r2hi)) {
+                            const double dx = (double)qx - (double)p[w].x, dy = (double)qy - (double)p[w].y,
+                                         dz = (double)qz - (double)p[w].z;
+                            const double d2 =
+                                __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
+                            in = d2 <= r2;
+                        }
+                        if (in) {
+                            if (m < cap) S.set(m, __float_as_uint(p[w].w));   // (the snapshot's w: original index)
+                            ++m;
                         }
                     }
                 }
+            }
+        }
     }
     cnt[i] = m;
     if (m > cap) {          // (the call replays with more slots; this row's result is discarded)
@@ -122,20 +171,20 @@ __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __res
     }
     // ascending original index: scipy's per-query order, the order the reference's scatter sums in
     for (int a = 1; a < m; ++a) {
-        const unsigned long long k = L[a * BSt];
+        const uint32_t k = S.get(a);
         int b = a - 1;
         for (; b >= 0; --b) {
-            const unsigned long long kb = L[b * BSt];
+            const uint32_t kb = S.get(b);
             if (kb <= k) break;
-            L[(b + 1) * BSt] = kb;
+            S.set(b + 1, kb);
         }
-        L[(b + 1) * BSt] = k;
+        S.set(b + 1, k);
     }
-    int32_t* R = rows + t0;
-    for (int t = 0; t < m; ++t) R[t * rm.nq] = (int32_t)(uint32_t)(L[t * BSt] & 0xFFFFFFFFull);
+    // original index -> snapshot row, into the row's slots of the member-row buffer (in place past L)
+    for (int t = 0; t < m; ++t) S.glb[t * rm.nq] = (uint32_t)inv[S.get(t)];
     const float4 n4 = nrm[i];
     const Vec3 ni = v3(n4.x, n4.y, n4.z);
-    const Sym3 T = nvt_normal_tensor(Rows4{nrm}, ni, m, LdsKeyNb{L, BSt}, rho);
+    const Sym3 T = nvt_normal_tensor(Rows4{nrm}, ni, m, RowNb{rows + t0, rm.nq}, rho);
     float w[3], V[3][3];
     eigh3(T, w, V);
     const Vec3 f = vu_smooth(w, V, ni, tau, damp);
@@ -173,15 +222,19 @@ __global__ void k_cpsd_maxcnt(const int32_t* __restrict__ cnt, RowMap rm, int* _
 
 }  // namespace pcd
 
-#ifndef PCD_CPSD_LDS_MAX
-#define PCD_CPSD_LDS_MAX 128
-#endif
-static constexpr int kCpsdLdsCap = PCD_CPSD_LDS_MAX;   // larger caps keep their slots in global memory (cgkeys)
+static constexpr int kCpsdLdsSlots = 32;   // member slots a lane keeps in LDS (4 B each; the rest in the row buffer)
+
+namespace pcd {
+__global__ void k_inv_perm(const int32_t* __restrict__ perm, int64_t n, int32_t* __restrict__ inv) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r < n) inv[perm[r]] = (int32_t)r;
+}
+}  // namespace pcd
 
 static void destroy_cpsd_state(pcd_denoiser* dn) {
     (void)hipFree(dn->ckeys); (void)hipFree(dn->ccnt); (void)hipFree(dn->covf);
-    (void)hipFree(dn->csave_pos); (void)hipFree(dn->csave_nrm); (void)hipFree(dn->cgkeys);
-    dn->ckeys = nullptr; dn->ccnt = nullptr; dn->covf = nullptr; dn->cgkeys = nullptr;
+    (void)hipFree(dn->csave_pos); (void)hipFree(dn->csave_nrm); (void)hipFree(dn->cinv);
+    dn->ckeys = nullptr; dn->ccnt = nullptr; dn->covf = nullptr; dn->cinv = nullptr;
     dn->csave_pos = dn->csave_nrm = nullptr;
     dn->cpsd_cap = 0;
 }
@@ -189,18 +242,15 @@ static void destroy_cpsd_state(pcd_denoiser* dn) {
 static int cpsd_alloc(pcd_denoiser* dn, int cap) {
     const int64_t N = dn->n;
     (void)hipFree(dn->ckeys);
-    (void)hipFree(dn->cgkeys);
     dn->ckeys = nullptr;
-    dn->cgkeys = nullptr;
     dn->cpsd_cap = 0;
     if (hipMalloc(&dn->ckeys, (size_t)N * (size_t)cap * sizeof(int32_t)) != hipSuccess)
         return fail(PCD_ERR_OOM, "pcd_cpsd_iterate: radius lists");
-    if (cap > kCpsdLdsCap && hipMalloc(&dn->cgkeys, (size_t)N * (size_t)cap * sizeof(unsigned long long)) != hipSuccess)
-        return fail(PCD_ERR_OOM, "pcd_cpsd_iterate: radius list slots");
     if (!dn->ccnt && (hipMalloc(&dn->ccnt, N * sizeof(int32_t)) != hipSuccess ||
                       hipMalloc(&dn->covf, sizeof(int)) != hipSuccess ||
                       hipMalloc(&dn->csave_pos, N * sizeof(float4)) != hipSuccess ||
-                      hipMalloc(&dn->csave_nrm, N * sizeof(float4)) != hipSuccess))
+                      hipMalloc(&dn->csave_nrm, N * sizeof(float4)) != hipSuccess ||
+                      hipMalloc(&dn->cinv, N * sizeof(int32_t)) != hipSuccess))
         return fail(PCD_ERR_OOM, "pcd_cpsd_iterate: buffers");
     dn->cpsd_cap = cap;
     return PCD_OK;
@@ -231,6 +281,9 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
     if (dn->cpsd_cap == 0 && (rc = cpsd_alloc(dn, 16)) != PCD_OK) return rc;
     const int64_t N = dn->n;
     const RowMap rm = dn->rowmap();
+    PCD_CHECK_ARG(dn->g && dn->g->n == N, "the denoiser's grid does not index its rows");
+    // original index -> snapshot row (the sort key back to the row the member lists hold)
+    hipLaunchKernelGGL(k_inv_perm, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, st, dn->g->perm, N, dn->cinv);
     // the state this call starts from (a replay after a radius-list overflow restarts from it)
     PCD_HIP(hipMemcpyAsync(dn->csave_pos, dn->pos[dn->cur], N * sizeof(float4), hipMemcpyDeviceToDevice, st));
     PCD_HIP(hipMemcpyAsync(dn->csave_nrm, dn->nrm, N * sizeof(float4), hipMemcpyDeviceToDevice, st));
@@ -248,15 +301,9 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
                 const int cap = dn->cpsd_cap;
 #define PCD_CPSD_NVT(C, B)                                                                                             \
     hipLaunchKernelGGL((k_cpsd_nvt<C, B>), dim3((unsigned)cdiv(rm.nq, B)), dim3(B), 0, st, gv, dn->pos[dn->cur], dn->nrm, \
-                       N, rm, cp->r, cp->rho, cp->tau, cp->damp, dn->ckeys, dn->ccnt, dn->fn, dn->covf, dn->cgkeys, cap)
-                // LDS slots cost occupancy (cap x 8 B a lane): past 16 slots they pay only on a launch too small to
-                // fill the chip anyway (A/B: 50k points 0.23 LDS vs 0.29 ms global; 1M at 64 slots 1.79 vs 1.42 ms)
-                const bool lds = cap <= 16 || (cap <= kCpsdLdsCap && rm.nq <= (int64_t)1 << 18);
-                if (!lds) PCD_CPSD_NVT(0, 128);
-                else if (cap == 16) PCD_CPSD_NVT(16, 128);
-                else if (cap == 32) PCD_CPSD_NVT(32, 128);
-                else if (cap == 64) PCD_CPSD_NVT(64, 64);
-                else PCD_CPSD_NVT(128, 64);
+                       N, rm, cp->r, cp->rho, cp->tau, cp->damp, dn->ckeys, dn->ccnt, dn->fn, dn->covf, dn->cinv, cap)
+                if (cap <= 16) PCD_CPSD_NVT(16, kCpsdBS);
+                else PCD_CPSD_NVT(kCpsdLdsSlots, kCpsdBS);
 #undef PCD_CPSD_NVT
                 hipLaunchKernelGGL(k_cpsd_pvt, grd, blk, 0, st, dn->pos[dn->cur], dn->fn, N, rm, cp->rho, cp->tau,
                                    dn->ckeys, cap, dn->ccnt, dn->cls, dn->edge);

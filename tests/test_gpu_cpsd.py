@@ -196,3 +196,34 @@ def test_cpsd_fused_equals_op_by_op(cpsd, gpu, rscale):
     dev = np.linalg.norm(out[True] - out[False], axis=1) / bbox
     print(f"rscale {rscale}: exact {np.mean(dev == 0):.4f} p99.9 {np.percentile(dev, 99.9):.3g} max {dev.max():.3g}")
     assert np.percentile(dev, 99.9) <= 1e-6 and np.median(dev) <= 1e-7, (np.percentile(dev, 99.9), np.median(dev))
+
+
+@pytest.mark.parametrize("rscale", [1.0, 1.8], ids=["r_d_lds_slots", "r_1.8d_global_slots"])
+def test_cpsd_fused_equals_op_by_op_large_cloud(gpu, rscale):
+    """The fused driver on a cloud past 2^18 rows (300k bunny-sampled points, bench.make_cloud): there the member
+    slots grow into global memory once a selection needs more than 16 (r = 1.8 d: ~50 members), at r = d they stay in
+    LDS.  One iteration against the op-by-op drop-in path within 1e-6 x bbox."""
+    from bench import make_cloud
+    pos0, n0, _ = make_cloud(300_000, 7, gpu)
+    bbox = float(torch.linalg.norm(pos0.max(0).values - pos0.min(0).values))
+    d = 2 * float(Processor(Pointcloud(pos0.clone(), n0.clone()), k_hint=16).meanEdgeLength())
+    out = {}
+    for fused in (True, False):
+        proc = Processor(Pointcloud(pos0.clone(), n0.clone()), k_hint=16)
+        if rscale != 1.0:
+            proc.getMartinFeatureDecomposition = (lambda f: (lambda r, rho=0.9: f(r * rscale, rho)))(
+                proc.getMartinFeatureDecomposition)
+        if fused:
+            import pcd_native as nat
+            dn = proc._fused_for(8)
+            dn.load(proc.graph.pos, proc.graph.n)
+            dn.cpsd_iterate(nat.make_cpsd_params(r=d * rscale, d=d), 1)
+            p = torch.empty_like(proc.graph.pos)
+            dn.store(p)
+            out[fused] = p.cpu().numpy()
+        else:
+            proc.cpsdDenoise(iterations=1, d=d, fused=False)
+            out[fused] = proc.graph.pos.cpu().numpy()
+    dev = np.linalg.norm(out[True] - out[False], axis=1) / bbox
+    print(f"large rscale {rscale}: exact {np.mean(dev == 0):.4f} p99.9 {np.percentile(dev, 99.9):.3g} max {dev.max():.3g}")
+    assert np.percentile(dev, 99.9) <= 1e-6 and np.median(dev) <= 1e-7, (np.percentile(dev, 99.9), np.median(dev))
