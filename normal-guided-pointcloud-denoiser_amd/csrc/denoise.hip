@@ -307,6 +307,9 @@ static constexpr int kAnchorBS = PCD_ANCHOR_BS;
 #ifndef PCD_ANCHOR_MAP24
 #define PCD_ANCHOR_MAP24 0
 #endif
+#ifndef PCD_ANCHOR_SPLIT
+#define PCD_ANCHOR_SPLIT 0
+#endif
 #ifndef PCD_ANCHOR_BATCH
 #define PCD_ANCHOR_BATCH 64   // anchor-set slots gathered per batch (all of them by default)
 #endif
@@ -342,14 +345,77 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
             const float S = 67108864.f / fmaxf(R * R, 1e-30f);
             uint32_t c[KA];
             int below = 0;
-            // the set's ranks and rows in batches of AB slots (AB = KA: every gather in flight at once; a smaller batch
-            // holds fewer rows in registers, a scheduling barrier keeping the next batch's loads behind this one's keys)
-            constexpr int AB = PCD_ANCHOR_BATCH < KA ? PCD_ANCHOR_BATCH : KA;
-            static_assert(KA % AB == 0 && AB % 8 == 0, "whole 8-column blocks per batch");
 #if PCD_ANCHOR_MAP24
             uint32_t base = 0;
             bool span_ok = true;
 #endif
+            // slot t -> snapshot rank rt into the LDS map
+            auto map_store = [&](int t, uint32_t rt) {
+#if PCD_ANCHOR_MAP24
+                const uint32_t dl = rt - base;
+                span_ok = span_ok && dl < (1u << 24);
+                s_lo[t * kAnchorBS + threadIdx.x] = (uint16_t)dl;
+                s_hi[t * kAnchorBS + threadIdx.x] = (uint8_t)(dl >> 16);
+#else
+                s_r[t * kAnchorBS + threadIdx.x] = rt;
+#endif
+            };
+            if constexpr (PCD_ANCHOR_SPLIT && KA == 64) {
+            // two halves of 32 slots: the second half's gathers are in flight while the first half's keys sort; the
+            // sorted halves merge by a half-cleaner (its low side: the 32 smallest, bitonic; its high side's minimum:
+            // the 33rd) and a 32-wide bitonic merge -- the same first kstore + 1 keys as the 64-key network
+            uint32_t ca[32], cb[32];
+            auto half = [&](int h, uint32_t (&cc)[32], auto&& between) {
+                uint32_t r[32];
+#pragma unroll
+                for (int g8 = 0; g8 < 4; ++g8) {
+                    const v4i* lp = lblock(alist, N, i, 4 * h + g8);
+                    const v4i x = __builtin_nontemporal_load(lp), y = __builtin_nontemporal_load(lp + 1);
+                    r[8 * g8 + 0] = (uint32_t)x.x; r[8 * g8 + 1] = (uint32_t)x.y; r[8 * g8 + 2] = (uint32_t)x.z;
+                    r[8 * g8 + 3] = (uint32_t)x.w; r[8 * g8 + 4] = (uint32_t)y.x; r[8 * g8 + 5] = (uint32_t)y.y;
+                    r[8 * g8 + 6] = (uint32_t)y.z; r[8 * g8 + 7] = (uint32_t)y.w;
+                }
+#if PCD_ANCHOR_MAP24
+                if (h == 0) base = min(r[0], (uint32_t)N);    // (the set is stored in rank order: its smallest rank)
+#endif
+                float4 pj[32];
+#pragma unroll
+                for (int u = 0; u < 32; ++u) {
+                    const uint32_t rt = min(r[u], (uint32_t)N);
+                    map_store(32 * h + u, rt);
+                    pj[u] = *at32(g.pts, rt);
+                }
+                between();
+#pragma unroll
+                for (int u = 0; u < 32; ++u) {
+                    const float d2 = dist2(vi, pj[u]);
+                    below += d2 < T ? 1 : 0;
+                    cc[u] = ((uint32_t)fminf(d2 * S, 67108860.f) << 6) | (uint32_t)(32 * h + u);
+                }
+            };
+            half(0, ca, [] {});
+            half(1, cb, [&] { oddeven_sort<32>(ca); });
+            oddeven_sort<32>(cb);
+            uint32_t c33 = 0xFFFFFFFFu;
+#pragma unroll
+            for (int u = 0; u < 32; ++u) {
+                const uint32_t lo = min(ca[u], cb[31 - u]), hi = max(ca[u], cb[31 - u]);
+                ca[u] = lo;
+                c33 = min(c33, hi);
+            }
+#pragma unroll
+            for (int d = 16; d > 0; d >>= 1)
+#pragma unroll
+                for (int u = 0; u < 32; ++u)
+                    if ((u & d) == 0) cswap(ca[u], ca[u + d]);
+#pragma unroll
+            for (int u = 0; u < 32; ++u) c[u] = ca[u];
+            c[32] = c33;
+            } else {
+            // the set's ranks and rows in batches of AB slots (AB = KA: every gather in flight at once; a smaller batch
+            // holds fewer rows in registers, a scheduling barrier keeping the next batch's loads behind this one's keys)
+            constexpr int AB = PCD_ANCHOR_BATCH < KA ? PCD_ANCHOR_BATCH : KA;
+            static_assert(KA % AB == 0 && AB % 8 == 0, "whole 8-column blocks per batch");
 #pragma unroll
             for (int b0 = 0; b0 < KA; b0 += AB) {
                 uint32_t r[AB];
@@ -370,14 +436,7 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
                     // an unused slot of a partial anchor set holds N: the snapshot's +inf sentinel row (the min keeps
                     // any entry inside the allocation)
                     const uint32_t rt = min(r[u], (uint32_t)N);
-#if PCD_ANCHOR_MAP24
-                    const uint32_t dl = rt - base;
-                    span_ok = span_ok && dl < (1u << 24);
-                    s_lo[t * kAnchorBS + threadIdx.x] = (uint16_t)dl;
-                    s_hi[t * kAnchorBS + threadIdx.x] = (uint8_t)(dl >> 16);
-#else
-                    s_r[t * kAnchorBS + threadIdx.x] = rt;
-#endif
+                    map_store(t, rt);
                     const float d2 = dist2(vi, *at32(g.pts, rt));   // unconditional load: the batch's gathers in flight
                     below += d2 < T ? 1 : 0;
                     // clamp below 2^26 in fp32 (2^26 - 1 rounds UP to 2^26, which would wrap to 0 after the shift);
@@ -387,6 +446,7 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
                 if (AB < KA) __builtin_amdgcn_sched_barrier(0);
             }
             PCD_ANCHOR_SORT<KA>(c);
+            }
             bool ok = below >= kstore;
 #if PCD_ANCHOR_MAP24
             ok = ok && span_ok;
