@@ -308,7 +308,7 @@ static constexpr int kAnchorBS = PCD_ANCHOR_BS;
 #define PCD_ANCHOR_MAP24 0
 #endif
 #ifndef PCD_ANCHOR_SPLIT
-#define PCD_ANCHOR_SPLIT 0
+#define PCD_ANCHOR_SPLIT 1   // 0: one 64-key network; 2: four quarters (A/B at 10M: anchor test 1.29 / 1.26 / 1.31 ms at 0 / 1 / 2)
 #endif
 #ifndef PCD_ANCHOR_BATCH
 #define PCD_ANCHOR_BATCH 64   // anchor-set slots gathered per batch (all of them by default)
@@ -360,7 +360,70 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
                 s_r[t * kAnchorBS + threadIdx.x] = rt;
 #endif
             };
-            if constexpr (PCD_ANCHOR_SPLIT && KA == 64) {
+            if constexpr (PCD_ANCHOR_SPLIT == 2 && KA == 64) {
+            // four quarters of 16 slots, each quarter's gathers in flight while the previous quarter's keys sort; the
+            // sorted quarters merge pairwise (bitonic, 32 each), then as in the two-halves variant
+            uint32_t qa[16], qb[16], qc[16], qd[16], ma[32], mb[32];
+            auto quarter = [&](int h, uint32_t (&cc)[16], auto&& between) {
+                uint32_t r[16];
+#pragma unroll
+                for (int g8 = 0; g8 < 2; ++g8) {
+                    const v4i* lp = lblock(alist, N, i, 2 * h + g8);
+                    const v4i x = __builtin_nontemporal_load(lp), y = __builtin_nontemporal_load(lp + 1);
+                    r[8 * g8 + 0] = (uint32_t)x.x; r[8 * g8 + 1] = (uint32_t)x.y; r[8 * g8 + 2] = (uint32_t)x.z;
+                    r[8 * g8 + 3] = (uint32_t)x.w; r[8 * g8 + 4] = (uint32_t)y.x; r[8 * g8 + 5] = (uint32_t)y.y;
+                    r[8 * g8 + 6] = (uint32_t)y.z; r[8 * g8 + 7] = (uint32_t)y.w;
+                }
+#if PCD_ANCHOR_MAP24
+                if (h == 0) base = min(r[0], (uint32_t)N);    // (the set is stored in rank order: its smallest rank)
+#endif
+                float4 pj[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const uint32_t rt = min(r[u], (uint32_t)N);
+                    map_store(16 * h + u, rt);
+                    pj[u] = *at32(g.pts, rt);
+                }
+                between();
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const float d2 = dist2(vi, pj[u]);
+                    below += d2 < T ? 1 : 0;
+                    cc[u] = ((uint32_t)fminf(d2 * S, 67108860.f) << 6) | (uint32_t)(16 * h + u);
+                }
+            };
+            // two sorted 16-runs -> one sorted 32-run: the second reversed makes the pair bitonic
+            auto merge16 = [](const uint32_t (&x)[16], const uint32_t (&y)[16], uint32_t (&z)[32]) {
+#pragma unroll
+                for (int u = 0; u < 16; ++u) { z[u] = x[u]; z[16 + u] = y[15 - u]; }
+#pragma unroll
+                for (int d = 16; d > 0; d >>= 1)
+#pragma unroll
+                    for (int u = 0; u < 32; ++u)
+                        if ((u & d) == 0) cswap(z[u], z[u + d]);
+            };
+            quarter(0, qa, [] {});
+            quarter(1, qb, [&] { oddeven_sort<16>(qa); });
+            quarter(2, qc, [&] { oddeven_sort<16>(qb); merge16(qa, qb, ma); });
+            quarter(3, qd, [&] { oddeven_sort<16>(qc); });
+            oddeven_sort<16>(qd);
+            merge16(qc, qd, mb);
+            uint32_t c33 = 0xFFFFFFFFu;
+#pragma unroll
+            for (int u = 0; u < 32; ++u) {
+                const uint32_t lo = min(ma[u], mb[31 - u]), hi = max(ma[u], mb[31 - u]);
+                ma[u] = lo;
+                c33 = min(c33, hi);
+            }
+#pragma unroll
+            for (int d = 16; d > 0; d >>= 1)
+#pragma unroll
+                for (int u = 0; u < 32; ++u)
+                    if ((u & d) == 0) cswap(ma[u], ma[u + d]);
+#pragma unroll
+            for (int u = 0; u < 32; ++u) c[u] = ma[u];
+            c[32] = c33;
+            } else if constexpr (PCD_ANCHOR_SPLIT == 1 && KA == 64) {
             // two halves of 32 slots: the second half's gathers are in flight while the first half's keys sort; the
             // sorted halves merge by a half-cleaner (its low side: the 32 smallest, bitonic; its high side's minimum:
             // the 33rd) and a 32-wide bitonic merge -- the same first kstore + 1 keys as the 64-key network
