@@ -716,8 +716,11 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
 #ifndef PCD_NVT2_NORM
 #define PCD_NVT2_NORM false
 #endif
+#ifndef PCD_NVT2_OCC
+#define PCD_NVT2_OCC 1
+#endif
 template <int K>
-__global__ __launch_bounds__(kNvtBS) void k_nvt2(const float4* __restrict__ pos, const float4* __restrict__ fn,
+__global__ __launch_bounds__(kNvtBS, PCD_NVT2_OCC) void k_nvt2(const float4* __restrict__ pos, const float4* __restrict__ fn,
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                float rho, float scale, uint8_t* __restrict__ cls,
                                                float4* __restrict__ edge, int win, float4* __restrict__ probe,
@@ -964,8 +967,11 @@ struct SplitRows {
     }
 };
 
+#ifndef PCD_PHASE_OCC
+#define PCD_PHASE_OCC 1
+#endif
 template <int KIND, int KU>
-__global__ __launch_bounds__(256) void k_phase(const float4* __restrict__ pin, float4* __restrict__ pout,
+__global__ __launch_bounds__(256, PCD_PHASE_OCC) void k_phase(const float4* __restrict__ pin, float4* __restrict__ pout,
                                                 const float4* __restrict__ fn, const float4* __restrict__ edge,
                                                 const int32_t* __restrict__ idx, int64_t N, RowMap rm, int ku,
                                                 const uint8_t* __restrict__ cls, int c, const float* __restrict__ g,
@@ -1193,6 +1199,9 @@ static int select_rows(pcd_denoiser* dn, const RowMap& rm, int32_t* list, unsign
 // Anchored K1 (seeded, list cap K <= 32, KA = 2K): the anchor test for every active row, then the re-anchoring
 // search (pcd_qknn.h) of the rows that failed it -- or of every row when there are no anchors (of this KA) yet --
 // and the exact-key wave search (pcd_wknn.h) for the few rows it spills.
+#ifndef PCD_RQ_Q
+#define PCD_RQ_Q 0             // steady re-anchoring: queries per wave sharing one scan (0: k_knn_requery, one)
+#endif
 #ifndef PCD_RQ_WD
 #define PCD_RQ_WD PCD_RQ_W     // lanes per query of the one-query dense launch (PCD_DENSE_Q = 0)
 #endif
@@ -1273,8 +1282,12 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
                 PCD_HIP(hipEventRecord(dn->join, dn->side));                                                           \
             }                                                                                                          \
             if (ev) PCD_HIP(hipEventRecord(ev[1], st));                                                                \
-            hipLaunchKernelGGL((k_knn_requery<2 * C, false>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, 0.f, dn->anc,  \
-                               dn->alist, dn->idx, dn->redo, redo_cnt, dn->spill, spill_cnt);                         \
+            if (PCD_RQ_Q > 0)                                                                                          \
+                hipLaunchKernelGGL((k_knn_dense_q<2 * C, (PCD_RQ_Q > 0 ? PCD_RQ_Q : 1), true>), grd_rq, blk, 0, st, gv, P, N, \
+                                   rm, kstore, 0.f, dn->anc, dn->alist, dn->idx, dn->spill, spill_cnt, dn->redo, redo_cnt); \
+            else                                                                                                       \
+                hipLaunchKernelGGL((k_knn_requery<2 * C, false>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, 0.f, dn->anc, \
+                                   dn->alist, dn->idx, dn->redo, redo_cnt, dn->spill, spill_cnt);                     \
         }                                                                                                              \
         if (ev) PCD_HIP(hipEventRecord(ev[2], st));                                                                    \
         hipLaunchKernelGGL((k_knn_redo_wave<2 * C, false>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,       \

@@ -737,14 +737,19 @@ PCD_DEV void rq_scan_box_q(const GridView& g, const Src& src, const Vec3 (&q)[Q]
 #define PCD_DENSE_Q 2        // queries per wave of the dense first anchoring (0: one, k_knn_requery<KA, true>; A/B at 10M: first iteration 23.6 / 21.8 / 25.4 ms at 0 / 2 / 4)
 #endif
 #ifndef PCD_DQ_OCC
-#define PCD_DQ_OCC 4
+#define PCD_DQ_OCC 6          // A/B at 10M: first iteration 21.7 / 20.7 / 21.3 ms at 4 (5 by VGPRs) / 6 / 7 waves per SIMD
 #endif
-template <int KA, int Q>
+// LIST (steady re-anchoring): the rows of list[0 .. *list_cnt) (the anchor test's failures, in row order, so
+// consecutive entries are spatial neighbours) with the radius of their old anchor, as k_knn_requery<KA, false>; a row
+// without an anchor spills to the wave search.
+template <int KA, int Q, bool LIST = false>
 __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, const float4* __restrict__ pos, int64_t N,
                                                                 RowMap rm, int kstore, float r_scale,
                                                                 float4* __restrict__ anc, int32_t* __restrict__ alist,
                                                                 int32_t* __restrict__ idx, int32_t* __restrict__ spill,
-                                                                unsigned* __restrict__ spill_cnt) {
+                                                                unsigned* __restrict__ spill_cnt,
+                                                                const int32_t* __restrict__ list = nullptr,
+                                                                const unsigned* __restrict__ list_cnt = nullptr) {
     constexpr int W = 64;
     __shared__ unsigned long long s_buf[4][Q][RqSurv<W>::n];
     __shared__ RqCells s_cells[4];
@@ -752,7 +757,8 @@ __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, con
     const LaneGrp<W> lg(lane);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
-    for (int64_t t0 = (lb * 4 + wv) * Q; t0 < rm.nq; t0 += (int64_t)gridDim.x * 4 * Q) {
+    const int64_t nrows = LIST ? (int64_t)*list_cnt : rm.nq;
+    for (int64_t t0 = (lb * 4 + wv) * Q; t0 < nrows; t0 += (int64_t)gridDim.x * 4 * Q) {
         int64_t iq[Q];
         Vec3 q[Q];
         float rs[Q];
@@ -764,16 +770,26 @@ __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, con
         bool any_big = false;
 #pragma unroll
         for (int j = 0; j < Q; ++j) {
-            act[j] = t0 + j < rm.nq;
-            iq[j] = (int64_t)rfl((uint32_t)rm(act[j] ? t0 + j : t0));
+            act[j] = t0 + j < nrows;
+            const int64_t tj = act[j] ? t0 + j : t0;
+            iq[j] = (int64_t)rfl((uint32_t)(LIST ? (int64_t)list[tj] : rm(tj)));
             const float4 p4 = pos[iq[j]];
             q[j] = v3(p4.x, p4.y, p4.z);
-            const int cx = min(max(cell_coord(q[j].x, g.ox, g.inv_h), 0), g.dx - 1);
-            const int cy = min(max(cell_coord(q[j].y, g.oy, g.inv_h), 0), g.dy - 1);
-            const int cz = min(max(cell_coord(q[j].z, g.oz, g.inv_h), 0), g.dz - 1);
-            uint32_t s = 0, e = 0;
-            const int n = cell_range(g, cx, cy, cz, s, e) ? (int)(e - s) : 1;
-            rs[j] = r_scale * g.h * cbrtf(16.f / (float)n);
+            if constexpr (LIST) {
+                const float4 a = anc[iq[j]];
+                if (!(a.w > 0.f)) {                     // no anchor: the wave search grows its own box
+                    if (act[j] && lg.hl == 0) spill[atomicAdd(spill_cnt, 1u)] = (int32_t)iq[j];
+                    act[j] = false;
+                }
+                rs[j] = a.w > 0.f ? a.w * PCD_RQ_RSCALE : g.h;
+            } else {
+                const int cx = min(max(cell_coord(q[j].x, g.ox, g.inv_h), 0), g.dx - 1);
+                const int cy = min(max(cell_coord(q[j].y, g.oy, g.inv_h), 0), g.dy - 1);
+                const int cz = min(max(cell_coord(q[j].z, g.oz, g.inv_h), 0), g.dz - 1);
+                uint32_t s = 0, e = 0;
+                const int n = cell_range(g, cx, cy, cz, s, e) ? (int)(e - s) : 1;
+                rs[j] = r_scale * g.h * cbrtf(16.f / (float)n);
+            }
             cap[j] = ((unsigned long long)__float_as_uint(rs[j] * rs[j]) << 32) | 0xFFFFFFFFull;
             int l3[3], h3[3];
             cell_box(g, q[j], rs[j] * 1.0001f + 1e-30f, l3, h3);
