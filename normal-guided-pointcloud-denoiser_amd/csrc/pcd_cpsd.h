@@ -27,6 +27,13 @@ static constexpr int kCpsdBS = 128;
 #define PCD_CPSD_CELLS 4
 #endif
 static constexpr int kCpsdCells = PCD_CPSD_CELLS;   // box cells looked up together by a lane
+#ifndef PCD_CPSD_NET
+#define PCD_CPSD_NET 1
+#endif
+#ifndef PCD_CPSD_ROWS
+#define PCD_CPSD_ROWS 8
+#endif
+static constexpr int kCpsdRows = PCD_CPSD_ROWS;     // candidate rows a lane has in flight
 
 struct RowNb {              // slot-major member rows: slot t at L[t * stride]
     const int32_t* L;
@@ -135,30 +142,39 @@ __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __res
                 cr[u] = make_uint2(0u, 0u);
                 if (brick != ~0u) cr[u] = g.cells[(uint64_t)brick * 64 + loc6[u]];
             }
+            // the chunk's rows as one stream across its cells (kCpsdRows loads in flight, whatever the cells' sizes)
+            uint32_t pre[kCpsdCells + 1];
+            pre[0] = 0;
 #pragma unroll
-            for (int u = 0; u < kCpsdCells; ++u) {
-                const uint2 ce = cr[u];
-                for (uint32_t r0 = ce.x; r0 < ce.y; r0 += 4) {
-                    float4 p[4];
+            for (int u = 0; u < kCpsdCells; ++u) pre[u + 1] = pre[u] + (cr[u].y > cr[u].x ? cr[u].y - cr[u].x : 0u);
+            const uint32_t total = pre[kCpsdCells];
+            for (uint32_t b0 = 0; b0 < total; b0 += kCpsdRows) {
+                float4 p[kCpsdRows];
 #pragma unroll
-                    for (int w = 0; w < 4; ++w) p[w] = g.pts[min(r0 + (uint32_t)w, ce.y - 1u)];   // 4 rows in flight
+                for (int w = 0; w < kCpsdRows; ++w) {
+                    const uint32_t j = min(b0 + (uint32_t)w, total - 1u);
+                    uint32_t row = 0;
 #pragma unroll
-                    for (int w = 0; w < 4; ++w) {
-                        if (r0 + (uint32_t)w >= ce.y) break;
-                        const float fx = qx - p[w].x, fy = qy - p[w].y, fz = qz - p[w].z;
-                        const float d2f = (fx * fx + fy * fy) + fz * fz;
-                        bool in = d2f < r2lo;
-                        if (!in && !(d2f > r2hi)) {
-                            const double dx = (double)qx - (double)p[w].x, dy = (double)qy - (double)p[w].y,
-                                         dz = (double)qz - (double)p[w].z;
-                            const double d2 =
-                                __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
-                            in = d2 <= r2;
-                        }
-                        if (in) {
-                            if (m < cap) S.set(m, __float_as_uint(p[w].w));   // (the snapshot's w: original index)
-                            ++m;
-                        }
+                    for (int u = 0; u < kCpsdCells; ++u)
+                        if (j >= pre[u] && j < pre[u + 1]) row = cr[u].x + (j - pre[u]);
+                    p[w] = g.pts[row];
+                }
+#pragma unroll
+                for (int w = 0; w < kCpsdRows; ++w) {
+                    if (b0 + (uint32_t)w >= total) break;
+                    const float fx = qx - p[w].x, fy = qy - p[w].y, fz = qz - p[w].z;
+                    const float d2f = (fx * fx + fy * fy) + fz * fz;
+                    bool in = d2f < r2lo;
+                    if (!in && !(d2f > r2hi)) {
+                        const double dx = (double)qx - (double)p[w].x, dy = (double)qy - (double)p[w].y,
+                                     dz = (double)qz - (double)p[w].z;
+                        const double d2 =
+                            __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
+                        in = d2 <= r2;
+                    }
+                    if (in) {
+                        if (m < cap) S.set(m, __float_as_uint(p[w].w));   // (the snapshot's w: original index)
+                        ++m;
                     }
                 }
             }
@@ -170,7 +186,27 @@ __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __res
         m = cap;
     }
     // ascending original index: scipy's per-query order, the order the reference's scatter sums in
+#if defined(PCD_EXP_CPSD) && PCD_EXP_CPSD >= 1      // timing experiment: no sort (sums in scan order: results differ)
+    if (m < 0)
+#endif
+    {
+#if PCD_CPSD_NET
+    // the LDS slots by a fixed network in registers (no chain of dependent LDS round trips; unused slots padded with
+    // the largest key), then the few overflow members (past L) inserted one by one
+    {
+        const int m0 = min(m, L);
+        uint32_t v[L];
+#pragma unroll
+        for (int t = 0; t < L; ++t) v[t] = t < m0 ? S.lds[t * S.bs] : 0xFFFFFFFFu;
+        oddeven_sort<L>(v);
+#pragma unroll
+        for (int t = 0; t < L; ++t)
+            if (t < m0) S.lds[t * S.bs] = v[t];
+    }
+    for (int a = L; a < m; ++a) {
+#else
     for (int a = 1; a < m; ++a) {
+#endif
         const uint32_t k = S.get(a);
         int b = a - 1;
         for (; b >= 0; --b) {
@@ -180,10 +216,14 @@ __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __res
         }
         S.set(b + 1, k);
     }
+    }
     // original index -> snapshot row, into the row's slots of the member-row buffer (in place past L)
     for (int t = 0; t < m; ++t) S.glb[t * rm.nq] = (uint32_t)inv[S.get(t)];
     const float4 n4 = nrm[i];
     const Vec3 ni = v3(n4.x, n4.y, n4.z);
+#if defined(PCD_EXP_CPSD) && PCD_EXP_CPSD >= 2      // timing experiment: no tensor / eigh (f_n = n)
+    if (m >= 0) { fn[i] = n4; return; }
+#endif
     const Sym3 T = nvt_normal_tensor(Rows4{nrm}, ni, m, RowNb{rows + t0, rm.nq}, rho);
     float w[3], V[3][3];
     eigh3(T, w, V);
