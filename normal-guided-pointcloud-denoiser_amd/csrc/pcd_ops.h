@@ -153,13 +153,26 @@ PCD_DEV Sym3 nvt_normal_tensor(Nr nrm, Vec3 ni, int cnt, Nb nb, float rho) {
     float w00 = 0.f, w01 = 0.f, w02 = 0.f, w11 = 0.f, w12 = 0.f, w22 = 0.f;
     int wsum = 0;
     const float crho = cosf(rho);
-    for (int t = 0; t < cnt; ++t) {
-        const Vec3 nj = nrm(nb(t));
-        const float c = fminf(fmaxf(dot3(ni, nj), -1.f), 1.f);
-        if (normal_vote(c, rho, crho)) {
-            w00 += nj.x * nj.x; w01 += nj.x * nj.y; w02 += nj.x * nj.z;
-            w11 += nj.y * nj.y; w12 += nj.y * nj.z; w22 += nj.z * nj.z;
-            ++wsum;
+    constexpr int B = 8;            // members in batches: every list entry, then every normal, in flight together
+    for (int t0 = 0; t0 < cnt; t0 += B) {
+        Vec3 nv[B];
+        {
+            int64_t j[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u) j[u] = nb(min(t0 + u, cnt - 1));
+#pragma unroll
+            for (int u = 0; u < B; ++u) nv[u] = nrm(j[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            if (t0 + u >= cnt) break;
+            const Vec3 nj = nv[u];
+            const float c = fminf(fmaxf(dot3(ni, nj), -1.f), 1.f);
+            if (normal_vote(c, rho, crho)) {
+                w00 += nj.x * nj.x; w01 += nj.x * nj.y; w02 += nj.x * nj.z;
+                w11 += nj.y * nj.y; w12 += nj.y * nj.z; w22 += nj.z * nj.z;
+                ++wsum;
+            }
         }
     }
     if (wsum == 0) return Sym3{ni.x * ni.x, ni.x * ni.y, ni.x * ni.z, ni.y * ni.y, ni.y * ni.z, ni.z * ni.z};
@@ -186,36 +199,63 @@ PCD_DEV Sym3 pvt_normal_cov(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, flo
         }
         return Sym3{a[0], a[1], a[2], a[3], a[4], a[5]};
     }
+    // members in batches of 8 (every list entry, then every gathered row of a batch in flight together); the votes
+    // of the first 64 members are kept as bits, so the centroid and covariance passes re-gather positions only.  Sums
+    // run over the voters in list order, as the reference's scatter.
+    constexpr int B = 8;
     int wsum = 0;
+    unsigned long long vbits = 0ull;
     const float crho = cosf(rho);
-    for (int t = 0; t < cnt; ++t) {
-        const float c = fminf(fmaxf(dot3(ni, nrm(nb(t))), -1.f), 1.f);
-        wsum += normal_vote(c, rho, crho) ? 1 : 0;
+    for (int t0 = 0; t0 < cnt; t0 += B) {
+        int64_t j[B];
+        Vec3 nj[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) j[u] = nb(min(t0 + u, cnt - 1));
+#pragma unroll
+        for (int u = 0; u < B; ++u) nj[u] = nrm(j[u]);
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            if (t0 + u >= cnt) break;
+            const float c = fminf(fmaxf(dot3(ni, nj[u]), -1.f), 1.f);
+            const bool v = normal_vote(c, rho, crho);
+            wsum += v ? 1 : 0;
+            if (v && t0 + u < 64) vbits |= 1ull << (t0 + u);
+        }
     }
     const bool all = wsum == 0;
     if (all) wsum = cnt;
-    auto vote = [&](int64_t j) {
+    auto vote = [&](int t, int64_t j) {
         if (all) return true;
+        if (t < 64) return ((vbits >> t) & 1ull) != 0ull;
         const float c = fminf(fmaxf(dot3(ni, nrm(j)), -1.f), 1.f);
         return normal_vote(c, rho, crho);
     };
+    // voters' positions of members t0 .. t0+B-1 -> f(vj) in list order
+    auto for_voters = [&](auto&& f) {
+        for (int t0 = 0; t0 < cnt; t0 += B) {
+            int64_t j[B];
+            Vec3 vj[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u) j[u] = nb(min(t0 + u, cnt - 1));
+#pragma unroll
+            for (int u = 0; u < B; ++u) vj[u] = pos(j[u]);
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                if (t0 + u >= cnt) break;
+                if (vote(t0 + u, j[u])) f(vj[u]);
+            }
+        }
+    };
     float sx = 0.f, sy = 0.f, sz = 0.f;
-    for (int t = 0; t < cnt; ++t) {
-        const int64_t j = nb(t);
-        if (!vote(j)) continue;
-        const Vec3 vj = pos(j);
-        sx += vj.x; sy += vj.y; sz += vj.z;
-    }
+    for_voters([&](Vec3 vj) { sx += vj.x; sy += vj.y; sz += vj.z; });
     const float c = (float)wsum;
     const Vec3 ctr = v3(sx / c, sy / c, sz / c);
     float a00 = 0.f, a01 = 0.f, a02 = 0.f, a11 = 0.f, a12 = 0.f, a22 = 0.f;
-    for (int t = 0; t < cnt; ++t) {
-        const int64_t j = nb(t);
-        if (!vote(j)) continue;
-        const Vec3 d = pos(j) - ctr;   // T[a][b] = dv[b] * dv[a] (wij[...,None] * dv[:,None] * dv[...,None])
+    for_voters([&](Vec3 vj) {
+        const Vec3 d = vj - ctr;   // T[a][b] = dv[b] * dv[a] (wij[...,None] * dv[:,None] * dv[...,None])
         a00 += d.x * d.x; a01 += d.y * d.x; a02 += d.z * d.x;
         a11 += d.y * d.y; a12 += d.z * d.y; a22 += d.z * d.z;
-    }
+    });
     return Sym3{a00 / c, a01 / c, a02 / c, a11 / c, a12 / c, a22 / c};
 }
 
