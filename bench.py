@@ -1,7 +1,11 @@
 """Benchmark: Mpoints/s per denoise iteration (kNN + NVT/PCA + update) at k = 32 on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--points P] [--k 32] [--k-update 8]
-    torchrun --nproc-per-node N ... bench.py --gpus N          (one process per GPU; weak scaling)
+
+--gpus N > 1 launches the N ranks itself (one process per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set for
+each) before anything touches a GPU, and refuses to run on a box with fewer than N GPUs unless --rehearse-one-gpu
+puts every rank on GPU 0 (libpcd's host-callback transport instead of RCCL).  Launched by torchrun instead
+(WORLD_SIZE already set), each process is one rank as it stands.
 
 Workload (BASELINE.json configs[3], the headline): `xyzrgb_dragon.obj` is a missing blob in the reference, so
 the substitute of BASELINE.md is used -- P (default 10,000,000) area-weighted samples of stanford-bunny.obj
@@ -10,18 +14,20 @@ One "step" = one full iteration of Processor.denoise's loop body on device-resid
 frozen snapshot -> NVT1 + VU smoothing -> NVT2 + classes -> flat (global reduce) / edge / corner updates.
 Excluded (one-time): snapshot/grid build, initial normals, mean edge length l, data synthesis.
 
-Multi-GPU (BASELINE configs[4]): one global cloud of N x P points is cut into N spatial slabs
-along its longest axis; each rank denoises its slab and exchanges halo state with its slab neighbours over RCCL
-(pcd_slab), plus two scalar all-reduces per flat phase -- weak scaling (P points per GPU).  --replicas instead
-runs N independent P-point clouds.  The timed region is bracketed by barrier + synchronize and the max over
-ranks is reported.
+Multi-GPU (BASELINE configs[4]): one global cloud of N x P points, made on rank 0 (the coordinator,
+the only process that holds it), is cut into N spatial slabs along its longest axis; rank 0 hands every rank its slab
++ halo over libpcd's RCCL communicator, each rank denoises its slab and exchanges halo rows with its slab neighbours
+(pcd_slab_iterate: RCCL over xGMI, plus two scalar all-reduces per flat phase) -- weak scaling (P points per GPU).
+torch.distributed is a gloo group for control only.  --replicas instead runs N independent P-point clouds.  The
+timed region is bracketed by barrier + synchronize and the max over ranks is reported; the slab coverage check of
+the timed iterations runs right after it (a thin halo re-plans and the region is timed again).
 
 The JSON line carries `roofline` for the dominant stage (K1 = kNN + NVT1, HIP events on its launch stream),
 `kernel_ms` per stage (HIP events), `ten_iteration_ms` (a fresh cloud through configs[3]'s 10 iterations, the dense
 first anchoring included), `measured_traffic` (the rocprofv3 PMC bytes of profiles/traffic.json per iteration against
-8 TB/s), `cpu_baseline` (the oracle restatement on host cores over a bounded sample) and `parity` (the same sample
-through one GPU iteration: Chamfer distance to the clean surface vs the oracle's, class agreement); the last two on
-rank 0 at N = 1 only.
+8 TB/s, null when that file was measured on another build of libpcd), `cpu_baseline` (the oracle restatement on host
+cores over a bounded sample) and `parity` (the same sample through one GPU iteration: Chamfer distance to the clean
+surface vs the oracle's, class agreement); the last two on rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
@@ -306,6 +312,30 @@ def slab_world1_bench(pos, nrm, params, args, fused_ms):
     return out
 
 
+def n1_point(args, dev):
+    """The single-GPU fused loop on args.points points (seed 2, the N = 1 bench's cloud): warm-up, then the timed
+    steps between synchronisations."""
+    pos, nrm, _ = make_cloud(args.points, 2, dev)
+    proc = Processor(Pointcloud(pos, nrm), k_hint=args.k)
+    d = 2 * float(proc.meanEdgeLength())
+    fused = proc._fused_for(max(args.k, args.k_update))
+    fused.load(proc.graph.pos, proc.graph.n)
+    params = nat.make_params(k=args.k, k_update=args.k_update, d=d)
+    fused.iterate(params, args.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fused.iterate(params, args.steps)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / args.steps * 1e3
+    fused.check()
+    out = {"points": args.points, "ms_per_step": round(ms, 4), "value": round(args.points / ms / 1e3, 3),
+           "unit": "Mpoints/s", "note": "rank 0 alone, single-GPU fused loop, same per-GPU point count, after the "
+                                        "slab run (its state still resident)"}
+    del fused, proc
+    torch.cuda.empty_cache()
+    return out
+
+
 def measured_traffic(points, k, ms_per_step):
     """HBM bytes per iteration from profiles/traffic.json (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch, the
     gfx950 correction of MI355X_MICROARCH.md), summed over the iteration's kernels, against 8 TB/s."""
@@ -318,10 +348,51 @@ def measured_traffic(points, k, ms_per_step):
         return None
     if tj.get("points") != points or tj.get("k") != k or "per_iteration_bytes" not in tj:
         return None
+    if tj.get("build_id") != nat.build_id():
+        return {"bytes_per_iteration": None, "frac": None, "traffic_build": tj.get("build_id"),
+                "lib_build": nat.build_id(), "note": "profiles/traffic.json was measured on another build of libpcd"}
     b = float(tj["per_iteration_bytes"])
-    return {"bytes_per_iteration": b, "achieved": round(b / (ms_per_step / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+    return {"bytes_per_iteration": b, "traffic_build": tj["build_id"],
+            "achieved": round(b / (ms_per_step / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(b / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "kind": TRAFFIC_KIND,
             "source": tj.get("source", "profiles/traffic.json")}
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int, rehearse: bool) -> int:
+    """--gpus N > 1 without a launcher: start N rank processes of this script (nothing here has touched a GPU) and
+    return the first non-zero exit status (the others are then stopped), else 0."""
+    import subprocess
+    have = torch.cuda.device_count()          # (counting devices does not initialise one)
+    if have < n and not rehearse:
+        print(f"bench.py: --gpus {n} needs {n} GPUs, this box has {have} (--rehearse-one-gpu puts every rank on "
+              f"GPU 0 over libpcd's host transport)", file=sys.stderr, flush=True)
+        return 2
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc, alive = 0, set(range(n))
+    while alive:
+        for r in sorted(alive):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            alive.discard(r)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in alive:
+                    procs[q].terminate()
+        time.sleep(0.1)
+    return rc
 
 
 def main():
@@ -355,47 +426,52 @@ def main():
                     help="skip the slab_world1 block (the multi-GPU driver at one rank on the same workload)")
     ap.add_argument("--no-ten", dest="ten", action="store_false",
                     help="skip the ten_iteration_ms measurement (fresh cloud, 10 iterations incl. the first)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N > 1: every rank on GPU 0, libpcd's host-callback transport over gloo instead of RCCL "
+                         "(a rehearsal of the multi-GPU path on a one-GPU box; not a scaling number)")
+    ap.add_argument("--no-n1", dest="n1", action="store_false",
+                    help="N > 1: skip the N = 1 comparison point (rank 0 alone, the same per-GPU workload)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, args.rehearse_one_gpu))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    local = local % max(1, torch.cuda.device_count())
+    if world > 1 and args.gpus != world and rank == 0:
+        print(f"bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr, flush=True)
+    if world > 1 and not args.rehearse_one_gpu and torch.cuda.device_count() < world:
+        print(f"bench.py: {world} ranks need {world} GPUs, this box has {torch.cuda.device_count()}",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    local = 0 if args.rehearse_one_gpu else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        # RCCL ("nccl") between GPUs; PCD_BENCH_BACKEND=gloo only to rehearse several ranks on one GPU
-        backend = os.environ.get("PCD_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        # control plane only (plan scalars, verdicts, the timing max); the data plane is libpcd's communicator
+        dist.init_process_group("gloo")
     mode = "single" if world == 1 else ("replicas" if args.replicas else "slab")
 
     if mode == "slab":
-        # one global cloud of world x P points (identical on every rank), cut into spatial slabs with a halo
+        # one global cloud of world x P points, made and held by rank 0 only (the coordinator), cut into spatial slabs
+        # with a halo; d = 2 l (Processor.py:120-121) likewise on rank 0 -- the other ranks never see the whole cloud
         from pcd_slab import SlabDenoiser, TorchTransport
         total = args.points if args.strong else args.points * world
-        # one cloud, sampled on rank 0 only and broadcast (device sampling is not bit-reproducible across ranks);
-        # d = 2 l (Processor.py:120-121) likewise on rank 0 only: the other ranks never grid the whole cloud
+        pos = nrm = None
+        dt = torch.zeros(1, dtype=torch.float64)
         if rank == 0:
             pos, nrm, diag = make_cloud(total, 3, dev)
-            dt = torch.tensor([2 * float(Processor(Pointcloud(pos), k_hint=args.k).meanEdgeLength())], device=dev)
-        else:
-            pos = torch.empty((total, 3), dtype=torch.float32, device=dev)
-            nrm = torch.empty_like(pos)
-            dt = torch.zeros(1, device=dev)
-        dist.broadcast(pos, 0)
-        dist.broadcast(nrm, 0)
+            dt[0] = 2 * float(Processor(Pointcloud(pos), k_hint=args.k).meanEdgeLength())
         dist.broadcast(dt, 0)
         d = float(dt)
         # coverage checked every 10 iterations (a thin halo re-plans and replays, pcd_slab); slabs re-cut by class
         # cost after the second warm-up iteration (rebalance), so the timed region runs on the balanced plan
-        sd = SlabDenoiser(pos, nrm, max(args.k, args.k_update), transport=TorchTransport(),
-                          seeding=args.seeding, check_every=10)
+        tr = TorchTransport(rccl=not args.rehearse_one_gpu)
+        sd = SlabDenoiser(pos, nrm, max(args.k, args.k_update), transport=tr, seeding=args.seeding, check_every=10)
         del pos, nrm
+        torch.cuda.empty_cache()
         params = nat.make_params(k=args.k, k_update=args.k_update, d=d)
         step = lambda: sd.iterate(params, 1)  # noqa: E731
     else:
@@ -424,22 +500,40 @@ def main():
             sd.rebalance()         # cost-weighted cut from this iteration's classes (next iteration re-anchors)
     if mode != "slab":
         fused.set_timing(True)     # per-stage HIP events on the launch stream, every timed iteration
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+
+    def timed_region():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t)
+        return el
+
+    if mode == "slab":
+        # the timed iterations carry no coverage check (a host sync + an all-reduce): it runs right after them, and a
+        # thin halo there (re-planned and replayed) sends the region round again on the widened plan
+        every = sd.check_every
+        for _attempt in range(3):
+            sd.checkpoint()
+            sd.check_every = args.steps + 1
+            replans = sd.replans
+            elapsed = timed_region()
+            sd.verify()
+            sd.check_every = every
+            if sd.replans == replans:
+                break
+    else:
+        elapsed = timed_region()
     ms_per_step = elapsed / args.steps * 1e3
     total_points = args.points if (mode == "slab" and args.strong) else args.points * world
     value = total_points / (ms_per_step / 1e3) / 1e6
@@ -509,12 +603,13 @@ def main():
     k1_bytes = b_alg_knn_nvt1(args.k) * k1_points
     achieved = k1_bytes / (knn_ms / 1e3) / 1e9 if knn_ms == knn_ms else None
     k1_names = k1_kernels(args.k, args.k_update, args.seeding, args.anchoring)
-    traffic = None
+    traffic, traffic_build = None, None
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile) and mode != "slab":
         try:
             tj = json.load(open(tfile))
-            if tj.get("points") == args.points and tj.get("k") == args.k:
+            traffic_build = tj.get("build_id")
+            if tj.get("points") == args.points and tj.get("k") == args.k and tj.get("build_id") == nat.build_id():
                 per = [tj["kernels"][nm][0]["hbm_bytes_per_launch"] for nm in k1_names if nm in tj["kernels"]]
                 traffic = float(sum(per)) if per else None
         except Exception:
@@ -560,7 +655,7 @@ def main():
         "roofline": {"kernel": "K1 stage (kNN + NVT1): " + " + ".join(k1_names), "bound": "valu+latency",
                      "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": traffic, "traffic_kind": TRAFFIC_KIND,
+                     "traffic": traffic, "traffic_kind": TRAFFIC_KIND, "traffic_build": traffic_build,
                      "measured_frac": (round(traffic / (knn_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
                                        if traffic and knn_ms == knn_ms else None),
                      "alg_bytes_per_launch": k1_bytes, "avg_launch_ms": round(knn_ms, 4)},
@@ -569,8 +664,27 @@ def main():
                             "SURVEY §8(d) algorithmic-bytes model (each neighbour attribute read counted per use, "
                             "most of them served by LDS windows and L2), `measured_frac` the counted bytes"),
     }
-    if out["measured_traffic"]:
+    out["lib_build"] = nat.build_id()
+    if out["measured_traffic"] and out["measured_traffic"].get("frac") is not None:
         out["iteration_roofline"]["measured_frac"] = out["measured_traffic"]["frac"]
+    if mode == "slab":
+        info = sd.comm.info()
+        counts = torch.tensor([sd.owned_global.numel(), sd.halo_points], dtype=torch.int64)
+        allc = [torch.zeros_like(counts) for _ in range(world)]
+        dist.all_gather(allc, counts)
+        out["slab"] = {"world": info["world"], "transport": info["transport"],
+                       "owned_rows": [int(c[0]) for c in allc], "halo_rows": [int(c[1]) for c in allc],
+                       "halo": sd.halo, "replans": sd.replans, "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
+                       "note": ("every rank on GPU 0 over libpcd's host transport: a rehearsal, not a scaling number"
+                                if args.rehearse_one_gpu else
+                                "one GPU per rank, halo rows and the flat phase's scalars over libpcd's RCCL "
+                                "communicator (xGMI); gloo carries control only")}
+        if args.n1:
+            # the N = 1 comparison point: rank 0 alone runs the single-GPU fused loop on the per-GPU workload (the
+            # N = 1 bench's cloud, seed 2), timed like the main region; the other ranks wait
+            if rank == 0:
+                out["n1"] = n1_point(args, dev)
+            dist.barrier()
     if rank == 0 and world == 1 and args.slab1:
         out["slab_world1"] = slab_world1_bench(pos, nrm, params, args, ms_per_step)
     if rank == 0 and world == 1 and args.extras:

@@ -50,6 +50,8 @@ enum {
 };
 const char* pcd_last_error(void);
 int pcd_version(void);
+/* hash of the sources and flags this library was built from (16 hex digits), e.g. to match profiles to builds */
+const char* pcd_build_id(void);
 /* Largest k supported by the kNN kernels (register top-k lists). */
 int pcd_max_k(void);
 
@@ -318,6 +320,17 @@ int pcd_comm_id(void* id_out);
 int pcd_comm_create(const void* id, int world, int rank, pcd_comm** out);
 int pcd_comm_create_host(const pcd_host_transport* t, int world, int rank, pcd_comm** out);
 int pcd_comm_destroy(pcd_comm* c);
+/* world size, this rank, and the transport (PCD_COMM_RCCL / PCD_COMM_HOST) the communicator was made with */
+enum { PCD_COMM_HOST = 0, PCD_COMM_RCCL = 1 };
+int pcd_comm_info(const pcd_comm* c, int* world, int* rank, int* transport);
+/* Point-to-point bulk copy of DEVICE memory, stream-ordered: send send_bytes from `send` to rank send_peer and
+ * receive recv_bytes into `recv` from rank recv_peer (a peer of -1: nothing that way).  Byte counts are multiples of
+ * 4.  The slab driver's coordinator (rank 0, the only rank holding the whole cloud, as the reference's single process
+ * does: Processor.py:115-121) hands each rank its slab + halo of the snapshot with it, and collects the owned state
+ * for a re-plan.  RCCL: ncclSend / ncclRecv in one group.  Host transport: staged through host memory and handed to
+ * the exchange callback as ceil(bytes / 16) float4 rows.  Synchronises `stream` on the host transport only. */
+int pcd_comm_sendrecv(pcd_comm* c, int send_peer, const void* send, int64_t send_bytes, int recv_peer, void* recv,
+                      int64_t recv_bytes, void* stream);
 /* in-place all-reduce of device scalars (the flat phase's Σ and δ, Denoiser.py:106-107), stream-ordered */
 int pcd_allreduce_scalars(pcd_comm* c, void* buf, int count, int dtype, int op, void* stream);
 /* Halo routes of this rank's denoiser: for each of npeers peers (host arrays), n_send[q] own rows to send and

@@ -1130,6 +1130,7 @@ struct pcd_denoiser {
     int32_t* cinv = nullptr;                             // original index -> snapshot row (the grid's perm inverted)
     int* covf = nullptr;
     int cpsd_cap = 0;
+    int64_t cpsd_elems = 0;                              // ckeys' allocated entries (N x cpsd_cap)
     float4 *csave_pos = nullptr, *csave_nrm = nullptr;   // the state at the call's start (a replay after overflow)
     RowMap rowmap() const { return RowMap{rows, rows ? n_rows : n}; }
 };
@@ -1250,7 +1251,9 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     // Dense (no anchors): every row is re-anchored, then NVT1 runs over all rows.  Seeded: the anchor test, then
     // NVT1 of the certified rows on the side stream while this stream re-anchors the others (latency-bound wave
     // searches beside VALU-bound lane work), then NVT1 of the re-anchored rows, then the join.
-    const bool overlap = !dense && PCD_NVT1_OVERLAP;
+    // (never under the slab iteration -- its NVT1 waits for the halo exchange and marks the band, which the side
+    // stream's k_nvt1 / k_nvt1_list do not -- nor for the CPSD driver's lists-only K1)
+    const bool overlap = !dense && PCD_NVT1_OVERLAP && dn->nvt1_on && !before_nvt1 && !band.flag;
     if (overlap && !dn->side) {
         PCD_HIP(hipStreamCreateWithFlags(&dn->side, hipStreamNonBlocking));
         PCD_HIP(hipEventCreateWithFlags(&dn->fork, hipEventDisableTiming));

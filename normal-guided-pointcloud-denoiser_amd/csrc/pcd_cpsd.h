@@ -277,6 +277,17 @@ static void destroy_cpsd_state(pcd_denoiser* dn) {
     dn->ckeys = nullptr; dn->ccnt = nullptr; dn->covf = nullptr; dn->cinv = nullptr;
     dn->csave_pos = dn->csave_nrm = nullptr;
     dn->cpsd_cap = 0;
+    dn->cpsd_elems = 0;
+}
+
+// Every buffer the selected k_cpsd_nvt<L> / k_cpsd_pvt launch dereferences, sized for what it indexes: the member
+// slots past L (and every slot k_cpsd_pvt reads) live in ckeys at [t][nq] for t < cap, so ckeys must hold cap x nq;
+// counts, the inverse permutation and the save buffers hold N rows.  (Round 4's fault: a launch selector that sent
+// cap > 16 at nq > 2^18 to a variant keeping its slots in a buffer allocated only past 128 slots -- a null ckeys.)
+static bool cpsd_buffers_ok(const pcd_denoiser* dn, int L, int cap, int64_t nq) {
+    return dn->ckeys && dn->ccnt && dn->covf && dn->cinv && dn->csave_pos && dn->csave_nrm && cap == dn->cpsd_cap &&
+           L <= kCpsdLdsSlots && (cap <= 16 ? L == 16 : L == kCpsdLdsSlots && cap >= L) && nq <= dn->n &&
+           dn->cpsd_elems >= (int64_t)cap * nq;
 }
 
 static int cpsd_alloc(pcd_denoiser* dn, int cap) {
@@ -284,8 +295,10 @@ static int cpsd_alloc(pcd_denoiser* dn, int cap) {
     (void)hipFree(dn->ckeys);
     dn->ckeys = nullptr;
     dn->cpsd_cap = 0;
+    dn->cpsd_elems = 0;
     if (hipMalloc(&dn->ckeys, (size_t)N * (size_t)cap * sizeof(int32_t)) != hipSuccess)
         return fail(PCD_ERR_OOM, "pcd_cpsd_iterate: radius lists");
+    dn->cpsd_elems = N * (int64_t)cap;
     if (!dn->ccnt && (hipMalloc(&dn->ccnt, N * sizeof(int32_t)) != hipSuccess ||
                       hipMalloc(&dn->covf, sizeof(int)) != hipSuccess ||
                       hipMalloc(&dn->csave_pos, N * sizeof(float4)) != hipSuccess ||
@@ -339,6 +352,11 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
             const dim3 grd((unsigned)cdiv(rm.nq, kCpsdBS)), blk(kCpsdBS);
             if (rm.nq > 0) {
                 const int cap = dn->cpsd_cap;
+                const int L = cap <= 16 ? 16 : kCpsdLdsSlots;
+                if (!cpsd_buffers_ok(dn, L, cap, rm.nq)) {
+                    rc = fail(PCD_ERR_STATE, "pcd_cpsd_iterate: buffers do not cover the selected kernel variant");
+                    break;
+                }
 #define PCD_CPSD_NVT(C, B)                                                                                             \
     hipLaunchKernelGGL((k_cpsd_nvt<C, B>), dim3((unsigned)cdiv(rm.nq, B)), dim3(B), 0, st, gv, dn->pos[dn->cur], dn->nrm, \
                        N, rm, cp->r, cp->rho, cp->tau, cp->damp, dn->ckeys, dn->ccnt, dn->fn, dn->covf, dn->cinv, cap)
@@ -384,14 +402,26 @@ int pcd_cpsd_iterate(pcd_denoiser* dn, const pcd_cpsd_params* cp, int iterations
             }
             break;
         }
-        // a radius selection had more members than the list slots: restart from the saved state with twice the slots
-        const int cap = dn->cpsd_cap * 2;
-        PCD_CHECK_ARG(cap <= (1 << 20), "a radius selection holds more than 2^20 points");
-        if ((rc = cpsd_alloc(dn, cap)) != PCD_OK) return rc;
+        // a radius selection had more members than the list slots: back to the saved state first (so an error below
+        // leaves the state the call started from), then slots for the largest selection of the last pass -- the
+        // counts are exact past the slots -- and at least twice the old ones, and replay
         dn->cur = cur0;
         PCD_HIP(hipMemcpyAsync(dn->pos[dn->cur], dn->csave_pos, N * sizeof(float4), hipMemcpyDeviceToDevice, st));
         PCD_HIP(hipMemcpyAsync(dn->nrm, dn->csave_nrm, N * sizeof(float4), hipMemcpyDeviceToDevice, st));
         dn->unit_nrm = unit0;
+        int h = 0;
+        {
+            int* mx = dn->covf;
+            PCD_HIP(hipMemsetAsync(mx, 0, sizeof(int), st));
+            hipLaunchKernelGGL(k_cpsd_maxcnt, dim3((unsigned)std::min<int64_t>(cdiv(rm.nq, 256), 1024)), dim3(256), 0,
+                               st, dn->ccnt, rm, mx);
+            PCD_HIP(hipMemcpyAsync(&h, mx, sizeof(int), hipMemcpyDeviceToHost, st));
+            PCD_HIP(hipStreamSynchronize(st));
+        }
+        int64_t cap = (int64_t)dn->cpsd_cap * 2;
+        while (cap < h) cap *= 2;
+        PCD_CHECK_ARG(cap <= (1 << 20), "a radius selection holds more than 2^20 points");
+        if ((rc = cpsd_alloc(dn, (int)cap)) != PCD_OK) return rc;
     }
     return PCD_OK;
 }

@@ -229,6 +229,50 @@ int pcd_comm_destroy(pcd_comm* c) {
     return PCD_OK;
 }
 
+int pcd_comm_info(const pcd_comm* c, int* world, int* rank, int* transport) {
+    PCD_CHECK_ARG(c != nullptr, "null comm");
+    if (world) *world = c->world;
+    if (rank) *rank = c->rank;
+    if (transport) *transport = c->nccl ? PCD_COMM_RCCL : PCD_COMM_HOST;
+    return PCD_OK;
+}
+
+int pcd_comm_sendrecv(pcd_comm* c, int send_peer, const void* send, int64_t send_bytes, int recv_peer, void* recv,
+                      int64_t recv_bytes, void* stream) {
+    PCD_CHECK_ARG(c != nullptr, "null comm");
+    PCD_CHECK_ARG(send_peer >= -1 && send_peer < c->world && recv_peer >= -1 && recv_peer < c->world, "bad peer");
+    PCD_CHECK_ARG(send_bytes >= 0 && recv_bytes >= 0 && send_bytes % 4 == 0 && recv_bytes % 4 == 0,
+                  "byte counts must be non-negative multiples of 4");
+    const bool tx = send_peer >= 0 && send_bytes > 0, rx = recv_peer >= 0 && recv_bytes > 0;
+    PCD_CHECK_ARG((!tx || send) && (!rx || recv), "null buffer");
+    if (!tx && !rx) return PCD_OK;
+    hipStream_t st = as_stream(stream);
+    if (c->nccl) {
+        PCD_NCCL(ncclGroupStart());
+        if (tx) PCD_NCCL(ncclSend(send, (size_t)send_bytes, ncclChar, send_peer, c->nccl, st));
+        if (rx) PCD_NCCL(ncclRecv(recv, (size_t)recv_bytes, ncclChar, recv_peer, c->nccl, st));
+        PCD_NCCL(ncclGroupEnd());
+        return PCD_OK;
+    }
+    // host transport: one exchange callback over at most two peers, the payloads as whole float4 rows
+    const int64_t srows = tx ? (send_bytes + 15) / 16 : 0, rrows = rx ? (recv_bytes + 15) / 16 : 0;
+    std::vector<float4> hs((size_t)std::max<int64_t>(srows, 1)), hr((size_t)std::max<int64_t>(rrows, 1));
+    if (tx) PCD_HIP(hipMemcpyAsync(hs.data(), send, (size_t)send_bytes, hipMemcpyDeviceToHost, st));
+    PCD_HIP(hipStreamSynchronize(st));
+    std::vector<int> peers;
+    std::vector<int64_t> so(1, 0), ro(1, 0);
+    if (tx) { peers.push_back(send_peer); so.push_back(srows); ro.push_back(send_peer == recv_peer && rx ? rrows : 0); }
+    if (rx && !(tx && send_peer == recv_peer)) { peers.push_back(recv_peer); so.push_back(so.back()); ro.push_back(rrows); }
+    if (c->host.exchange(c->host.user, (int)peers.size(), peers.data(), reinterpret_cast<const float*>(hs.data()),
+                         so.data(), reinterpret_cast<float*>(hr.data()), ro.data()) != 0)
+        return fail(PCD_ERR_RCCL, "pcd_comm_sendrecv: host transport exchange callback failed");
+    if (rx) {
+        PCD_HIP(hipMemcpyAsync(recv, hr.data(), (size_t)recv_bytes, hipMemcpyHostToDevice, st));
+        PCD_HIP(hipStreamSynchronize(st));
+    }
+    return PCD_OK;
+}
+
 int pcd_allreduce_scalars(pcd_comm* c, void* buf, int count, int dtype, int op, void* stream) {
     PCD_CHECK_ARG(c != nullptr, "null comm");
     PCD_CHECK_ARG(count >= 0 && (count == 0 || buf), "null buffer");

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("PCD_LIB", os.path.join(os.path.dirname(_HERE), "libpc
 PCD_OK, PCD_ERR_ARG, PCD_ERR_OOM, PCD_ERR_HIP, PCD_ERR_STATE, PCD_ERR_RCCL = 0, -1, -2, -3, -4, -5
 DT_F32, DT_F64, DT_I32 = 0, 1, 2
 OP_SUM, OP_MAX = 0, 1
+COMM_HOST, COMM_RCCL = 0, 1
 FIELD_POS, FIELD_NRM, FIELD_FN, FIELD_EDGE = 0, 1, 2, 3
 (STAGE_KNN_NVT1, STAGE_NVT2, STAGE_PHASE_SUM, STAGE_PHASE_CENTRE, STAGE_PHASE_MAXDIST, STAGE_PHASE_APPLY,
  STAGE_FINISH) = range(7)
@@ -51,6 +52,7 @@ class DenoiseParams(ctypes.Structure):
 _SIGS = {
     "pcd_last_error": (ctypes.c_char_p, []),
     "pcd_version": (c_int, []),
+    "pcd_build_id": (ctypes.c_char_p, []),
     "pcd_max_k": (c_int, []),
     "pcd_denoise_params_size": (c_int, []),
     "pcd_grid_build": (c_int, [c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, POINTER(c_void_p)]),
@@ -110,6 +112,8 @@ _SIGS = {
     "pcd_comm_create": (c_int, [c_void_p, c_int, c_int, POINTER(c_void_p)]),
     "pcd_comm_create_host": (c_int, [c_void_p, c_int, c_int, POINTER(c_void_p)]),
     "pcd_comm_destroy": (c_int, [c_void_p]),
+    "pcd_comm_info": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
+    "pcd_comm_sendrecv": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_int, c_void_p, c_int64, c_void_p]),
     "pcd_allreduce_scalars": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "pcd_denoiser_set_routes": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p]),
@@ -147,6 +151,11 @@ def lib():
                               f"pcd_denoise_params is {L.pcd_denoise_params_size()} B -- rebuild or update the mirror")
         _lib = L
     return _lib
+
+
+def build_id() -> str:
+    """The loaded library's build id (pcd_build_id: a hash of its sources and extra flags)."""
+    return lib().pcd_build_id().decode()
 
 
 def exported_symbols():
@@ -525,6 +534,25 @@ class Comm:
         check(lib().pcd_comm_create_host(ctypes.byref(cbs), int(world), int(rank), ctypes.byref(h)),
               "pcd_comm_create_host")
         return Comm(h, keep=(cbs, _ex, _ar))
+
+    def info(self) -> dict:
+        """world / rank / transport ("rccl" or "host") as the library's communicator sees them (pcd_comm_info)."""
+        w, r, tr = c_int(0), c_int(0), c_int(0)
+        check(lib().pcd_comm_info(self.handle, ctypes.byref(w), ctypes.byref(r), ctypes.byref(tr)), "pcd_comm_info")
+        return {"world": w.value, "rank": r.value, "transport": "rccl" if tr.value == COMM_RCCL else "host"}
+
+    def sendrecv(self, send_peer: int = -1, send: torch.Tensor = None, recv_peer: int = -1,
+                 recv: torch.Tensor = None):
+        """Point-to-point copy of contiguous device tensors (pcd_comm_sendrecv): `send` to rank send_peer, `recv`
+        filled from rank recv_peer, in place; either side may be absent (peer -1)."""
+        for t in (send, recv):
+            assert t is None or (t.is_cuda and t.is_contiguous() and (t.numel() * t.element_size()) % 4 == 0)
+        sb = 0 if send is None else send.numel() * send.element_size()
+        rb = 0 if recv is None else recv.numel() * recv.element_size()
+        check(lib().pcd_comm_sendrecv(self.handle, int(send_peer if send is not None else -1), ptr(send), sb,
+                                      int(recv_peer if recv is not None else -1), ptr(recv), rb,
+                                      c_void_p(stream_ptr())), "pcd_comm_sendrecv")
+        return recv
 
     def allreduce_(self, t: torch.Tensor, op: int = OP_SUM) -> torch.Tensor:
         """In-place all-reduce of a small device tensor (float32 / float64 / int32)."""

@@ -107,42 +107,61 @@ class SlabPlan:
 
 # ----------------------------------------------------------------------------------------------- transport
 class TorchTransport:
-    """Halo exchange and scalar all-reduces over torch.distributed: NCCL (= RCCL on ROCm, over xGMI) moves device
-    tensors directly; gloo stages through host memory.  With NCCL, Work.wait() only makes the current (launch) stream
-    wait for the communication stream -- the exchanges stay stream-ordered and the host is not blocked; the halo
-    costs are measured per stage by SlabDenoiser.iterate_timed (fn_exchange, phases_with_exchange)."""
+    """The slab driver's CONTROL plane over a torch.distributed CPU group (gloo): the RCCL unique id, the few scalars
+    of the plan, the coverage verdicts.  The DATA plane is libpcd's own communicator (pcd_comm, native_comm): RCCL
+    over xGMI (rccl=True: one GPU per rank, the product path) or host callbacks over this gloo group (rccl=False:
+    ranks sharing one GPU, the tests and the one-GPU rehearsal).  There is exactly one RCCL communicator per process,
+    and it belongs to the library; an NCCL torch group is refused.  The staged path (SlabDenoiser(native=False))
+    exchanges halo rows over this group itself, staged through host memory."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, rccl: bool = False):
         import torch.distributed as dist
         self.dist = dist
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        self.host = dist.get_backend(group) == "gloo"
+        if dist.get_backend(group) != "gloo":
+            raise ValueError("pcd_slab: the control group must be gloo (CPU); RCCL is libpcd's own (pcd_comm) -- "
+                             "pass TorchTransport(rccl=True) for an RCCL data plane")
+        self.host = True
+        self.rccl = bool(rccl)
+        self._comm = None
 
     def exchange(self, sends: dict, recv_shapes: dict, device) -> dict:
         """sends: peer -> tensor; recv_shapes: peer -> shape.  Returns peer -> received tensor on `device`."""
         dist = self.dist
         ops, outs, staged = [], {}, {}
         for peer, shape in recv_shapes.items():
-            buf = torch.empty(shape, dtype=torch.float32, device="cpu" if self.host else device)
+            buf = torch.empty(shape, dtype=torch.float32)
             outs[peer] = buf
             ops.append(dist.P2POp(dist.irecv, buf, peer, self.group))
         for peer, t in sends.items():
-            staged[peer] = t.cpu() if self.host else t.contiguous()
+            staged[peer] = t.cpu()
             ops.append(dist.P2POp(dist.isend, staged[peer], peer, self.group))
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
-        return {p: (b.to(device) if self.host else b) for p, b in outs.items()}
+        return {p: b.to(device) for p, b in outs.items()}
+
+    def send(self, t: torch.Tensor, dst: int):
+        self.dist.send(t.contiguous().cpu(), dst, self.group)
+
+    def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        h = torch.empty(t.shape, dtype=t.dtype)
+        self.dist.recv(h, src, self.group)
+        t.copy_(h)
+        return t
 
     def native_comm(self) -> "nat.Comm":
-        """libpcd's transport for pcd_slab_iterate (collective): an RCCL communicator of its own when this group is
-        NCCL (= RCCL), else host callbacks over this (gloo) group -- the same library code path, each exchange staged
-        through pinned host memory."""
+        """libpcd's data plane for pcd_slab_iterate and the slab hand-out (collective on first use, then cached): an
+        RCCL communicator (rccl=True; its unique id travels over this gloo group), else host callbacks over this
+        group -- the same library code path, each exchange staged through pinned host memory."""
+        if self._comm is not None:
+            return self._comm
         dist, grp = self.dist, self.group
-        if not self.host:
-            return nat.Comm.rccl(self.world, self.rank, lambda t: self.broadcast_(t.to(nat.device()), 0).cpu())
+        if self.rccl:
+            self._comm = nat.Comm.rccl(self.world, self.rank, lambda t: self.broadcast_(t, 0))
+            return self._comm
 
         def exchange(peers, send, soff, recv, roff):
             ops = []
@@ -159,32 +178,29 @@ class TorchTransport:
             t = torch.from_numpy(buf)
             dist.all_reduce(t, dist.ReduceOp.MAX if op == nat.OP_MAX else dist.ReduceOp.SUM, grp)
 
-        return nat.Comm.host(self.world, self.rank, exchange, allreduce)
+        self._comm = nat.Comm.host(self.world, self.rank, exchange, allreduce)
+        return self._comm
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
-        if self.host and t.device.type != "cpu":
-            h = t.cpu()
-            self.dist.broadcast(h, src, self.group)
+        h = t.cpu() if t.device.type != "cpu" else t
+        self.dist.broadcast(h, src, self.group)
+        if h is not t:
             t.copy_(h)
-        else:
-            self.dist.broadcast(t, src, self.group)
         return t
 
     def all_reduce(self, t: torch.Tensor, op: str) -> torch.Tensor:
         dist = self.dist
         red = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX}[op]
-        if self.host and t.device.type != "cpu":
-            h = t.cpu()
-            dist.all_reduce(h, red, self.group)
+        h = t.cpu() if t.device.type != "cpu" else t
+        dist.all_reduce(h, red, self.group)
+        if h is not t:
             t.copy_(h)
-        else:
-            dist.all_reduce(t, red, self.group)
         return t
 
 
 class LocalTransport:
     """world = 1: nothing to exchange."""
-    rank, world = 0, 1
+    rank, world, host, rccl = 0, 1, True, False
 
     def exchange(self, sends, recv_shapes, device):
         assert not sends and not recv_shapes
@@ -284,15 +300,74 @@ class HipSlabEngine:
 
 
 # ----------------------------------------------------------------------------------------------- driver
+@dataclass
+class RankShare:
+    """One rank's share of a plan, as the coordinator hands it out: its local snapshot (owned + halo), the owned
+    rows, the halo routes (peer -> local indices to send / receive) and the boxes the engine checks and overlaps on."""
+    local: torch.Tensor                 # int64 [nl]: global ids, ascending
+    owned_local: torch.Tensor           # int64 [no]: local indices of the owned points, ascending
+    pos: torch.Tensor                   # float32 [nl, 3]: the frozen snapshot's rows
+    n: torch.Tensor                     # float32 [nl, 3]
+    peers: list
+    send_local: list                    # per peer: int64 local indices of own points the peer holds as halo
+    recv_local: list                    # per peer: int64 local indices of the peer's points held here as halo
+    coverage: tuple                     # (lo3, hi3): the slab widened by the halo
+    own_box: tuple | None               # (lo3, hi3): the owned slab, strict (None at world 1)
+    lattice: tuple                      # (origin3, cell) of the global cell lattice (HIP engine)
+    halo: float
+    axis: int
+    state: tuple | None = None          # (pos, n) [nl, 3] of the current iterate to take over (a re-plan)
+
+
+def _share(plan: SlabPlan, r: int, snap_pos, snap_n, lattice, state=None) -> RankShare:
+    """The coordinator's cut of `plan` for rank r (everything on snap_pos's device)."""
+    world = plan.world
+    local = plan.local[r]
+    owner_l = plan.owner[local]
+    owned_local = torch.nonzero(owner_l == r).flatten()
+    to_local = None
+    peers, send_local, recv_local = [], [], []
+    for q in range(world):
+        if q == r:
+            continue
+        out = plan.transfer(r, q)            # own points q holds (global, ascending)
+        inc = plan.transfer(q, r)            # q's points held here
+        if out.numel() == 0 and inc.numel() == 0:
+            continue
+        if to_local is None:
+            to_local = torch.full((plan.owner.numel(),), -1, dtype=torch.int64, device=local.device)
+            to_local[local] = torch.arange(local.numel(), device=local.device)
+        peers.append(q)
+        send_local.append(to_local[out])
+        recv_local.append(to_local[inc])
+    own_box = None
+    if peers:
+        # the OWNED slab, strict: a snapshot point ON a cut may be owned by the neighbour, so the box is shrunk by
+        # one float32 ulp on the cut faces (rows whose k-ball stays inside it read no halo row)
+        import numpy as np
+        big = 3.0e38
+        lo, hi = [-big] * 3, [big] * 3
+        if r > 0:
+            lo[plan.axis] = float(np.nextafter(np.float32(plan.lo[r]), np.float32(np.inf)))
+        if r < world - 1:
+            hi[plan.axis] = float(np.nextafter(np.float32(plan.hi[r]), np.float32(-np.inf)))
+        own_box = (lo, hi)
+    st = None if state is None else (state[0][local.to(state[0].device)], state[1][local.to(state[1].device)])
+    return RankShare(local, owned_local, snap_pos[local], snap_n[local], peers, send_local, recv_local,
+                     plan.coverage(r), own_box, lattice, plan.halo, plan.axis, st)
+
+
 class SlabDenoiser:
     """The body of Processor.denoise (Processor.py:119-139) over spatial slabs, one rank per GPU.
 
-    snap_pos / snap_n: the WHOLE cloud (the frozen snapshot is the initial positions, as in Selector.__init__);
-    rank 0's copy is broadcast, so every rank plans from identical data and keeps it (the frozen snapshot a re-plan
-    cuts again).  halo: slab widening in snapshot units (None: 3x the largest k-th neighbour distance of a sample,
-    see default_halo, estimated on rank 0 and broadcast).  check_every: iterations between coverage checks
-    (0: never -- check() raises at the caller's request instead); halo_growth / max_replans: the thin-halo
-    recovery."""
+    Rank 0 is the COORDINATOR, the one process that holds the whole cloud as the reference's single process does
+    (Processor.py:115-121): snap_pos / snap_n are read on rank 0 only (the other ranks may pass None).  It estimates
+    the halo, cuts the slabs, and hands every rank its share -- slab + halo rows of the frozen snapshot, owned rows,
+    routes -- over libpcd's communicator (pcd_comm_sendrecv: RCCL over xGMI in the product path).  No other rank ever
+    holds or plans over the whole cloud.  A re-plan (thin halo, rebalance) gathers the owned state to rank 0, which
+    cuts again and hands out the new shares.  halo: slab widening in snapshot units (None: default_halo, on rank 0).
+    check_every: iterations between coverage checks (0: never -- check() raises at the caller's request instead);
+    halo_growth / max_replans: the thin-halo recovery."""
 
     def __init__(self, snap_pos, snap_n, k_max, transport=None, halo=None, engine_factory=None, seeding=True,
                  k_hint=None, check_every=1, halo_growth=2.0, max_replans=4, weights=None, native=None):
@@ -300,17 +375,6 @@ class SlabDenoiser:
         False: the same stages driven from Python over torch.distributed."""
         self.t = transport or LocalTransport()
         rank, world = self.t.rank, self.t.world
-        if world > 1:
-            snap_pos = self.t.broadcast_(snap_pos.contiguous().clone())
-            snap_n = self.t.broadcast_(snap_n.contiguous().clone())
-        if halo is None:
-            # one rank grids the whole cloud for the estimate and broadcasts it (every rank planning from the same
-            # value; the others never build a grid over the global cloud)
-            h = torch.zeros(1, dtype=torch.float64, device=snap_pos.device)
-            if rank == 0:
-                h.fill_(default_halo(snap_pos, k_max))
-            halo = float(self.t.broadcast_(h)) if world > 1 else float(h)
-        self.snap_pos, self.snap_n = snap_pos, snap_n
         # cell lattice of the ranks' snapshot indices: the fused loop's (pcd_native.fused_k_hint) unless given
         self.k_max, self.k_hint, self.seeding = k_max, k_hint or nat.fused_k_hint(k_max) or 32, seeding
         self.engine_factory = engine_factory
@@ -319,125 +383,183 @@ class SlabDenoiser:
         self.check_every, self.halo_growth, self.max_replans = int(check_every), float(halo_growth), int(max_replans)
         self.replans = 0
         self.e = None
-        self._lattice = None
-        self._setup(SlabPlan.build(snap_pos, world, halo, weights=weights))
+        if rank == 0:
+            self.snap_pos, self.snap_n = snap_pos.detach().contiguous(), snap_n.detach().contiguous()
+            self.dev = self.snap_pos.device
+            if halo is None:
+                halo = default_halo(self.snap_pos, k_max)
+            self._lattice = (nat.grid_params(self.snap_pos.to(nat.device()), k_hint=self.k_hint)
+                             if engine_factory is None else ([0.0, 0.0, 0.0], 0.0))
+            plan = SlabPlan.build(self.snap_pos, world, halo, weights=weights)
+            nt = torch.tensor([self.snap_pos.size(0)], dtype=torch.int64)
+        else:
+            self.snap_pos = self.snap_n = None
+            self.dev = nat.device() if engine_factory is None else torch.device("cpu")
+            plan, nt = None, torch.zeros(1, dtype=torch.int64)
+        self.n_total = int(self.t.broadcast_(nt, 0)) if world > 1 else int(nt)
+        self.plan = plan                         # (the coordinator's; None on the other ranks)
+        self._setup(plan)
         self._since = 0            # iterations since the last checkpoint
         self._pending = []         # their params (replayed after a re-plan)
         self._ckpt = None
 
+    # -------------------------------------------------------------------------------- coordinator <-> ranks
+    def _p2p_send(self, t: torch.Tensor, dst: int):
+        if self.native:
+            self.comm.sendrecv(dst, t.contiguous().to(nat.device()), -1, None)
+        else:
+            self.t.send(t, dst)
+
+    def _p2p_recv(self, shape, dtype, src: int) -> torch.Tensor:
+        if self.native:
+            return self.comm.sendrecv(-1, None, src, torch.empty(shape, dtype=dtype, device=nat.device()))
+        return self.t.recv(torch.empty(shape, dtype=dtype, device=self.dev), src)
+
+    def _send_share(self, s: RankShare, dst: int):
+        """Four messages: a fixed header, the index arrays, the float64 boxes, the float32 rows."""
+        ints = [s.local, s.owned_local, torch.tensor(s.peers, dtype=torch.int64),
+                torch.tensor([x.numel() for x in s.send_local], dtype=torch.int64),
+                torch.tensor([x.numel() for x in s.recv_local], dtype=torch.int64)] + s.send_local + s.recv_local
+        ints = torch.cat([x.to(self.dev, torch.int64) for x in ints])
+        nan = float("nan")
+        own = s.own_box or ([nan] * 3, [nan] * 3)
+        flt = torch.tensor(list(s.coverage[0]) + list(s.coverage[1]) + list(own[0]) + list(own[1])
+                           + list(s.lattice[0]) + [s.lattice[1], s.halo, float(s.axis)], dtype=torch.float64)
+        cols = [s.pos, s.n] + (list(s.state) if s.state is not None else [])
+        rows = torch.cat([c.to(self.dev, torch.float32) for c in cols], 1)
+        head = torch.tensor([s.local.numel(), s.owned_local.numel(), len(s.peers), int(s.state is not None),
+                             ints.numel(), 0, 0, 0], dtype=torch.int64)
+        for t in (head, ints, flt, rows):
+            self._p2p_send(t, dst)
+
+    def _recv_share(self) -> RankShare:
+        head = self._p2p_recv((8,), torch.int64, 0).cpu().tolist()
+        nl, no, npeers, has_state, nints = head[:5]
+        ints = self._p2p_recv((nints,), torch.int64, 0).to(self.dev)
+        flt = self._p2p_recv((20,), torch.float64, 0).cpu().tolist()
+        rows = self._p2p_recv((nl, 12 if has_state else 6), torch.float32, 0).to(self.dev)
+        o = 0
+        local, o = ints[o:o + nl], o + nl
+        owned_local, o = ints[o:o + no], o + no
+        peers, o = ints[o:o + npeers].tolist(), o + npeers
+        ns, o = ints[o:o + npeers].tolist(), o + npeers
+        nr, o = ints[o:o + npeers].tolist(), o + npeers
+        send_local, recv_local = [], []
+        for c in ns:
+            send_local.append(ints[o:o + c])
+            o += c
+        for c in nr:
+            recv_local.append(ints[o:o + c])
+            o += c
+        own = None if flt[6] != flt[6] else (flt[6:9], flt[9:12])
+        st = (rows[:, 6:9], rows[:, 9:12]) if has_state else None
+        return RankShare(local, owned_local, rows[:, 0:3], rows[:, 3:6], peers, send_local, recv_local,
+                         (flt[0:3], flt[3:6]), own, (flt[12:15], flt[15]), flt[16], int(flt[17]), st)
+
+    def _gather_to0(self, x: torch.Tensor):
+        """Per-point values of every rank's own points (owned-local order, [n_own, c] float32) -> the global
+        [N, c] on the coordinator (None elsewhere).  The coordinator knows every rank's owned ids from its plan, so
+        only the values travel.  Collective."""
+        rank, world = self.t.rank, self.t.world
+        x = x.to(self.dev, torch.float32).contiguous()
+        if rank != 0:
+            self._p2p_send(x, 0)
+            return None
+        out = torch.empty((self.n_total, x.size(1)), dtype=torch.float32, device=self.dev)
+        out[self.owned_global.to(self.dev)] = x
+        for r in range(1, world):
+            ids = torch.nonzero(self.plan.owner == r).flatten().to(self.dev)
+            out[ids] = self._p2p_recv((ids.numel(), x.size(1)), torch.float32, r).to(self.dev)
+        return out
+
     # -------------------------------------------------------------------------------- plan -> engine + routes
     def _setup(self, plan, state=None):
-        """Build this rank's engine and halo routes for `plan`; state = (global pos, global n) of the CURRENT
-        iterate to take over (None: the snapshot itself, i.e. a fresh start)."""
+        """Hand out `plan` (coordinator) / take this rank's share, then build the engine and halo routes; state =
+        (global pos, global n) of the CURRENT iterate on the coordinator (None: the snapshot, a fresh start)."""
         rank, world = self.t.rank, self.t.world
-        self.plan = plan
-        self.local = plan.local[rank]                           # global ids, ascending
-        pos_l, n_l = self.snap_pos[self.local], self.snap_n[self.local]
-        owned_mask = plan.owner[self.local] == rank
-        self.owned_local = torch.nonzero(owned_mask).flatten()
-        self.owned_global = self.local[self.owned_local]
         self.e = None                                           # free the old engine's device state first
+        if rank == 0:
+            self.plan = plan
+            for r in range(1, world):
+                self._send_share(_share(plan, r, self.snap_pos, self.snap_n, self._lattice, state), r)
+            s = _share(plan, 0, self.snap_pos, self.snap_n, self._lattice, state)
+        else:
+            s = self._recv_share()
+        self.halo, self.axis = s.halo, s.axis
+        self.local = s.local
+        self.owned_local = s.owned_local
+        self.owned_global = self.local[self.owned_local]
         if self.engine_factory is None:
-            if self._lattice is None:
-                self._lattice = nat.grid_params(self.snap_pos.to(nat.device()), k_hint=self.k_hint)
-            origin, cell = self._lattice
-            self.e = HipSlabEngine(pos_l, n_l, self.owned_local, self.k_max, origin, cell, plan.coverage(rank),
+            self.e = HipSlabEngine(s.pos, s.n, self.owned_local, self.k_max, s.lattice[0], s.lattice[1], s.coverage,
                                    self.seeding)
         else:
-            self.e = self.engine_factory(pos_l, n_l, self.owned_local, self.k_max, plan.coverage(rank))
-        if state is not None:
+            self.e = self.engine_factory(s.pos, s.n, self.owned_local, self.k_max, s.coverage)
+        if s.state is not None:
             # the engine loaded the snapshot (its `orig` for the global clamp); the current iterate goes on top
-            lid = torch.arange(self.local.numel(), device=self.local.device)
-            self.e.set_state(lid, state[0][self.local.to(state[0].device)], state[1][self.local.to(state[1].device)])
+            self.e.set_state(torch.arange(self.local.numel(), device=self.local.device), s.state[0], s.state[1])
         # halo routes: rows I send to each peer and rows I receive from it (both ascending global index)
-        to_local = torch.full((self.snap_pos.size(0),), -1, dtype=torch.int64, device=self.local.device)
-        to_local[self.local] = torch.arange(self.local.numel(), device=self.local.device)
         self.send_rows, self.recv_rows = {}, {}
-        for peer in range(world):
-            if peer == rank:
-                continue
-            out = plan.transfer(rank, peer)
-            inc = plan.transfer(peer, rank)
-            if out.numel():
-                self.send_rows[peer] = self.e.rows(to_local[out])
-            if inc.numel():
-                self.recv_rows[peer] = self.e.rows(to_local[inc])
+        for q, peer in enumerate(s.peers):
+            if s.send_local[q].numel():
+                self.send_rows[peer] = self.e.rows(s.send_local[q])
+            if s.recv_local[q].numel():
+                self.recv_rows[peer] = self.e.rows(s.recv_local[q])
         self.halo_points = sum(r.numel() for r in self.recv_rows.values())
         if self.native:
-            # routes + the OWNED slab (the rows whose k-ball stays strictly inside it read no halo row: NVT2 / the
-            # phases run them while an exchange is in flight).  Strict bounds: a snapshot point ON a cut may be owned
-            # by the neighbour, so the box is shrunk by one float32 ulp on the cut faces.
-            import numpy as np
-            big = 3.0e38
-            lo, hi = [-big] * 3, [big] * 3
-            if rank > 0:
-                lo[plan.axis] = float(np.nextafter(np.float32(plan.lo[rank]), np.float32(np.inf)))
-            if rank < world - 1:
-                hi[plan.axis] = float(np.nextafter(np.float32(plan.hi[rank]), np.float32(-np.inf)))
+            # routes + the OWNED slab (NVT2 / the phases run the rows that read no halo row while an exchange is in
+            # flight)
             peers = sorted(set(self.send_rows) | set(self.recv_rows))
             empty = torch.zeros(0, dtype=torch.int32, device=nat.device())
+            own = s.own_box if peers else None
             self.e.set_routes(peers, [self.send_rows.get(q, empty) for q in peers],
-                              [self.recv_rows.get(q, empty) for q in peers], lo if peers else None,
-                              hi if peers else None)
+                              [self.recv_rows.get(q, empty) for q in peers], own[0] if own else None,
+                              own[1] if own else None)
 
     def _owned_state_now(self):
         """(pos, n) of this rank's own points, owned-local order (a checkpoint)."""
         rows = self.e.rows(self.owned_local)
         return self.e.pack(nat.FIELD_POS, rows)[:, :3].clone(), self.e.pack(nat.FIELD_NRM, rows)[:, :3].clone()
 
-    def _gather_owned(self, x: torch.Tensor) -> torch.Tensor:
-        """Per-point values of this rank's own points (owned-local order, [n_own, c] float32) -> the global [N, c]
-        on every rank.  Every rank knows the others' owned ids from the plan, so only the values travel (padded
-        all-gather).  Collective."""
-        n_tot = self.snap_pos.size(0)
-        dev = x.device
-        out = torch.empty((n_tot, x.size(1)), dtype=torch.float32, device=dev)
-        if self.t.world == 1:
-            out[self.owned_global.to(dev)] = x
-            return out
-        counts = torch.bincount(self.plan.owner, minlength=self.t.world).tolist()
-        cdev = "cpu" if self.t.host else dev
-        pay = torch.zeros((max(counts), x.size(1)), dtype=torch.float32, device=cdev)
-        pay[: x.size(0)] = x.to(cdev)
-        bufs = [torch.empty_like(pay) for _ in range(self.t.world)]
-        self.t.dist.all_gather(bufs, pay, self.t.group)
-        for r, b in enumerate(bufs):
-            ids = torch.nonzero(self.plan.owner == r).flatten().to(dev)
-            out[ids] = b[: counts[r]].to(dev)
-        return out
-
     def _global_state(self, owned_pos, owned_n):
-        g = self._gather_owned(torch.cat([owned_pos, owned_n], 1))
-        return g[:, :3], g[:, 3:]
+        g = self._gather_to0(torch.cat([owned_pos, owned_n], 1))
+        return None if g is None else (g[:, :3], g[:, 3:])
 
-    def _replan(self, halo=None, weights=None, state=None):
-        """Re-cut every rank from the frozen snapshot, taking over `state` (global current pos, n; default: the
-        present iterate).  Collective: all ranks call it together."""
-        if state is None:
+    def _replan(self, halo=None, weights=None, state="now"):
+        """Re-cut every rank from the frozen snapshot, taking over `state` (global current pos, n on the
+        coordinator, None on the other ranks; "now": gather the present iterate).  Collective: all ranks call it
+        together."""
+        if isinstance(state, str):
             state = self._global_state(*self._owned_state_now())
-        halo = self.plan.halo if halo is None else halo
-        self._setup(SlabPlan.build(self.snap_pos, self.t.world, halo, axis=self.plan.axis, weights=weights), state)
+        plan = None
+        if self.t.rank == 0:
+            halo = self.plan.halo if halo is None else halo
+            plan = SlabPlan.build(self.snap_pos, self.t.world, halo, axis=self.plan.axis, weights=weights)
+        self._setup(plan, state)
 
     def _any_rank(self, flag: bool) -> bool:
+        """Does any rank raise `flag`?  Through libpcd's communicator (pcd_allreduce_scalars) on the native path."""
         if self.t.world == 1:
             return flag
-        dev = "cpu" if self.t.host else self.snap_pos.device
-        f = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+        if self.native:
+            f = torch.tensor([1 if flag else 0], dtype=torch.int32, device=nat.device())
+            self.comm.allreduce_(f, nat.OP_MAX)
+            return bool(f.item())
+        f = torch.tensor([1 if flag else 0], dtype=torch.int32)
         self.t.all_reduce(f, "max")
         return bool(f.item())
 
     def _verify(self):
         """Coverage check of the iterations since the checkpoint; on a thin halo: restore the checkpoint, widen the
         halo, re-plan and replay them."""
-        gstate = None
         while self._any_rank(bool(self.e.status() & 2)):
             if self.replans >= self.max_replans:
                 raise nat.PcdError(f"pcd_slab: halo still too thin after {self.replans} re-plans "
-                                   f"(halo {self.plan.halo:.4g})")
-            if gstate is None:                  # (the checkpoint is in the order of the plan it was taken under)
-                gstate = self._global_state(*self._ckpt)
-            self._replan(self.plan.halo * self.halo_growth, state=gstate)
+                                   f"(halo {self.halo:.4g})")
+            # (the checkpoint is in the order of the plan it was taken under: gathered before the re-cut)
+            gstate = self._global_state(*self._ckpt)
+            self._replan(self.halo * self.halo_growth if self.t.rank == 0 else None, state=gstate)
             self.replans += 1
+            self._ckpt = self._owned_state_now()            # the restored checkpoint, in the new plan's order
             for p in self._pending:
                 self._one(p)
         self._pending = []
@@ -483,7 +605,7 @@ class SlabDenoiser:
 
     def iterate(self, params, iterations: int = 1):
         for _ in range(iterations):
-            if self.check_every > 0 and self._since == 0:
+            if self.check_every > 0 and self._ckpt is None:
                 self._ckpt = self._owned_state_now()
                 self._pending = []
             self._one(params)
@@ -491,23 +613,35 @@ class SlabDenoiser:
                 self._pending.append(params)
                 self._since += 1
                 if self._since >= self.check_every:
-                    self._verify()
-                    self._since = 0
+                    self.verify()
+
+    def verify(self):
+        """Check the iterations since the last checkpoint now (re-planning and replaying them on a thin halo); the
+        next iteration takes a fresh checkpoint.  Collective."""
+        if self._pending:
+            self._verify()
+        self._since, self._pending, self._ckpt = 0, [], None
+
+    def checkpoint(self):
+        """verify(), then checkpoint the present state at once, so that the next `check_every` iterations run
+        without taking one (the bench's timed region: no host synchronisation inside it).  Collective."""
+        self.verify()
+        if self.check_every > 0:
+            self._ckpt = self._owned_state_now()
 
     def rebalance(self, class_weights=(1.0, 1.3, 1.4)):
         """Re-cut the slabs by cost: each point weighs class_weights[its class in the last NVT2 stage] (flat, edge,
         corner: the edge / feature steps solve a 3x3 system over their neighbours).  Collective.  Iterations since the
         last coverage check are verified first (a thin halo there re-plans and replays them), so the state carried
         into the new cut is exact."""
-        if self.check_every > 0 and self._since > 0:
-            self._verify()
+        self.verify()
         cls = self.e.classes()
         cls = cls[self.owned_local.to(cls.device)]
         w_tab = torch.tensor(class_weights, dtype=torch.float32, device=cls.device)
         w_own = w_tab[cls.clamp(0, len(class_weights) - 1)]
-        weights = self._gather_owned(w_own[:, None])[:, 0].to(self.snap_pos.device)
-        self._replan(weights=weights)
-        self._since, self._pending = 0, []
+        weights = self._gather_to0(w_own[:, None])
+        self._replan(weights=None if weights is None else weights[:, 0].to(self.snap_pos.device))
+        self._since, self._pending, self._ckpt = 0, [], None
 
     def iterate_timed(self, params) -> dict:
         """One iteration with CUDA/HIP events on the launch stream around each stage group (ms)."""

@@ -301,7 +301,8 @@ def test_fused_iteration_matches_reference(fan, gpu):
     assert np.percentile(a, 99) < 1e-4 and (a < 1e-2).mean() > 0.998
     bbox = np.linalg.norm(fan["pos0"].max(0) - fan["pos0"].min(0))
     dev = np.linalg.norm(pos - fan["it1_pos_after_2"], axis=1) / bbox
-    assert np.percentile(dev, 99) < 3e-4 and np.median(dev) < 1e-6
+    print(f"fandisk 1 iteration: median {np.median(dev):.3g} p99 {np.percentile(dev, 99):.3g} max {dev.max():.3g}")
+    assert np.percentile(dev, 99) <= 1e-5 and np.median(dev) <= 1e-7
 
 
 @pytest.mark.parametrize("k,anchoring", [(8, True), (16, True), (32, True), (64, True), (16, False), (32, False)])
@@ -475,7 +476,8 @@ def test_thesis_driver_matches_reference(golden, gpu):
     proc.thesisDenoise(iterations=1, d=float(g["d"]))
     bbox = np.linalg.norm(g["pos0"].max(0) - g["pos0"].min(0))
     dev1 = np.linalg.norm(v.cpu().numpy() - g["pos_it1"], axis=1) / bbox
-    assert np.percentile(dev1, 99) < 3e-4 and np.median(dev1) < 1e-6
+    print(f"thesis 1 iteration: median {np.median(dev1):.3g} p99 {np.percentile(dev1, 99):.3g} max {dev1.max():.3g}")
+    assert np.percentile(dev1, 99) <= 1e-5 and np.median(dev1) <= 1e-7
     proc2 = Processor(Pointcloud(T(g["pos0"], gpu).clone(), T(g["n0"], gpu).clone()))
     proc2.thesisDenoise(iterations=2, d=float(g["d"]))
     dev2 = np.linalg.norm(proc2.graph.pos.cpu().numpy() - g["pos_it2"], axis=1) / bbox

@@ -6,7 +6,7 @@
   positions, normals and classes.  Any kNN list that differed would change the state (the loop is chaotic), so this
   pins the anchored lists, the re-anchoring searches and the window reads at the size the bench times.
 * a 200k-point sample of the same workload: one iteration against the CPU oracle (classes >= 99.8 %, p99 position
-  deviation <= 3e-4 x bbox, median <= 1e-6 x bbox -- the tolerances of test_gpu_parity's single-iteration check).
+  deviation <= 1e-5 x bbox, median <= 1e-7 x bbox -- the tolerances of test_gpu_parity's single-iteration check).
 * configs[0] (bunny vertices, sigma = 0.003 x bbox, seed 0, k = 16, 5 iterations): per-iteration Chamfer distance to the
   clean bunny against the oracle's, within 3x the oracle's own sensitivity to a 1e-6 perturbation of its input normals
   (measured in the test) plus 0.2 %.
@@ -121,14 +121,24 @@ def _one_iteration_vs_oracle(pos, nrm, k, dev):
     agree = float((gc.cpu().numpy() == rcls).mean())
     bbox = float(np.linalg.norm(p0.max(0) - p0.min(0)))
     dev_pos = np.linalg.norm(gp.cpu().numpy() - rpos, axis=1) / bbox
+    print(f"{N} points, 1 iteration vs the oracle: classes {agree:.6f} median {np.median(dev_pos):.3g} "
+          f"p99 {np.percentile(dev_pos, 99):.3g} p99.9 {np.percentile(dev_pos, 99.9):.3g} max {dev_pos.max():.3g}")
     assert agree >= 0.998, agree
-    assert np.percentile(dev_pos, 99) <= 3e-4 and np.median(dev_pos) <= 1e-6, (np.percentile(dev_pos, 99),
+    assert np.percentile(dev_pos, 99) <= 1e-5 and np.median(dev_pos) <= 1e-7, (np.percentile(dev_pos, 99),
                                                                               np.median(dev_pos))
 
 
 def test_headline_workload_sample_one_iteration_vs_oracle(gpu):
     """A 200k-point sample of the configs[3] workload: one fused iteration against the CPU oracle."""
     pos, nrm = bunny_cloud(200_000, 2, 0.005)
+    _one_iteration_vs_oracle(pos, nrm, 32, gpu)
+
+
+def test_headline_workload_1m_one_iteration_vs_oracle(gpu):
+    """The bench's `parity` sample (bench.cpu_baseline: 1M points of the headline workload, make_cloud seed 99 drawn
+    on the host): one fused iteration against the CPU oracle at the one-iteration gate."""
+    from bench import make_cloud
+    pos, nrm, _ = make_cloud(1_000_000, 99, torch.device("cpu"))
     _one_iteration_vs_oracle(pos, nrm, 32, gpu)
 
 

@@ -1,6 +1,7 @@
 """Spatial slabs on the GPU: the staged HIP engine against the one-GPU fused loop, with one rank,
-with two ranks sharing the box's GPU over gloo, and -- where at least two GPUs are visible -- two ranks on two GPUs
-over RCCL (backend "nccl"; skipped on a one-GPU box, the driver's 8-GPU bench exercises it at scale)."""
+with two ranks sharing the box's GPU over libpcd's host-callback transport on a gloo group, and -- where at least two
+GPUs are visible -- two ranks on two GPUs over libpcd's own RCCL communicator (skipped on a one-GPU box, the driver's
+8-GPU bench exercises it at scale).  Only rank 0 (the coordinator) ever holds the whole cloud."""
 import os
 import socket
 
@@ -67,20 +68,24 @@ def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=F
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dev = torch.device("cuda", rank if backend == "nccl" else 0)
+    # the control group is always gloo; backend "rccl" = libpcd's own RCCL communicator as the data plane (one GPU
+    # per rank), "gloo" = its host-callback transport (ranks sharing the box's GPU)
+    dev = torch.device("cuda", rank if backend == "rccl" else 0)
     torch.cuda.set_device(dev)
-    if backend == "nccl":
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-    else:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        c = np.load(cloud_path)
-        pos, nrm = torch.from_numpy(c["pos"]).to(dev), torch.from_numpy(c["n"]).to(dev)
-        tr = TorchTransport()
+        pos = nrm = None
+        if rank == 0:                   # only the coordinator holds the cloud
+            c = np.load(cloud_path)
+            pos, nrm = torch.from_numpy(c["pos"]).to(dev), torch.from_numpy(c["n"]).to(dev)
+        tr = TorchTransport(rccl=backend == "rccl")
         sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K, native=native)
+        if native is not False:
+            assert sd.comm.info() == {"world": world, "rank": rank,
+                                      "transport": "rccl" if backend == "rccl" else "host"}
         sd.iterate(_params(d, jacobi), ITERS)
         sd.check()
-        p, n = gather_global(sd.owned_state(), pos.size(0), tr)
+        p, n = gather_global(sd.owned_state(), sd.n_total, tr)
         if rank == 0:
             np.savez(out_path, pos=p.numpy(), n=n.numpy(), halo=sd.halo_points)
     finally:
@@ -168,8 +173,10 @@ def _worker_owned(rank, world, port, out_prefix, cloud_path, d, halo=None, iters
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        c = np.load(cloud_path)
-        pos, nrm = torch.from_numpy(c["pos"]).to(dev), torch.from_numpy(c["n"]).to(dev)
+        pos = nrm = None
+        if rank == 0:                   # only the coordinator holds the cloud
+            c = np.load(cloud_path)
+            pos, nrm = torch.from_numpy(c["pos"]).to(dev), torch.from_numpy(c["n"]).to(dev)
         tr = TorchTransport()
         sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K, halo=halo, check_every=check_every)
         del pos, nrm
@@ -180,7 +187,7 @@ def _worker_owned(rank, world, port, out_prefix, cloud_path, d, halo=None, iters
             sd.iterate(_params(d), rebalance_after)
             sd.rebalance()
             sd.iterate(_params(d), iters - rebalance_after)
-        sd._verify()                    # the iterations since the last check (the bench's exactness check)
+        sd.verify()                     # the iterations since the last check (the bench's exactness check)
         sd.check()
         ids, p, n = sd.owned_state()
         np.savez(f"{out_prefix}_{rank}.npz", ids=ids.cpu().numpy(), pos=p.cpu().numpy(), n=n.cpu().numpy(),
@@ -324,7 +331,8 @@ def test_hip_slab_world2_jacobi_matches_one_gpu(gpu, tmp_path):
 
 @pytest.mark.gpu
 def test_hip_slab_world2_rccl_two_gpus(gpu, tmp_path):
-    """Two ranks on two GPUs over RCCL (the bench's multi-GPU transport); needs >= 2 visible GPUs."""
+    """Two ranks on two GPUs over libpcd's RCCL communicator (the bench's multi-GPU data plane; gloo control group);
+    needs >= 2 visible GPUs."""
     if torch.cuda.device_count() < 2:
         pytest.skip("needs two GPUs (RCCL ranks cannot share one device)")
     import torch.multiprocessing as mp
@@ -332,7 +340,7 @@ def test_hip_slab_world2_rccl_two_gpus(gpu, tmp_path):
     d = _d(pos)
     out, cloud = str(tmp_path / "slab2r.npz"), str(tmp_path / "cloud.npz")
     np.savez(cloud, pos=pos.cpu().numpy(), n=nrm.cpu().numpy())
-    mp.spawn(_worker, args=(2, _free_port(), out, cloud, d, "nccl"), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), out, cloud, d, "rccl"), nprocs=2, join=True)
     res = np.load(out)
     assert int(res["halo"]) > 0
     rp, rn = _fused(pos, nrm, d)
@@ -347,3 +355,24 @@ def test_default_halo_covers_knn(gpu):
     h = default_halo(pos, K)
     _, d2 = nat.Grid(pos, k_hint=K).knn(pos, K, with_d2=True)
     assert h >= 2.9 * float(d2[:, -1].max().sqrt())
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_self_launch_rehearsal():
+    """`bench.py --gpus 2` launches its two ranks itself (no torchrun), here both on the box's one GPU over libpcd's
+    host transport (--rehearse-one-gpu): the line reports two ranks, spatial slabs, libpcd's own view of the world,
+    every point owned once and a halo on both ranks."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--rehearse-one-gpu", "--points", "400000", "--steps", "3",
+           "--warmup", "3", "--no-extras", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    print({k: line[k] for k in ("value", "ms_per_step", "n_gpus")}, line["slab"], line.get("n1"))
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "spatial slabs x2"
+    assert line["slab"]["world"] == 2 and line["slab"]["transport"] == "host"
+    assert sum(line["slab"]["owned_rows"]) == 800_000 and min(line["slab"]["halo_rows"]) > 0
+    assert line["n1"]["points"] == 400_000 and line["value"] > 0

@@ -137,13 +137,15 @@ def check_stages(got, ref_cls, ref_fn, ref_eig2, ref_edge, ref_after, knn, pos0,
     knn_ok = (got["knn"][:, :KU] == nb).all(1)
     dec_ok = cls_ok & cls_ok[nb].all(1) & fn_same & fn_same[nb].all(1) & nb_fn_ok & knn_ok
     # the chained variant (own f_n, own edge vectors, own positions after the previous phase) feeds each phase inputs
-    # that differ from the reference's by rounding: a phase's own arithmetic is gated where its CONTINUOUS inputs agree
+    # that differ from the reference's by rounding.  Its gate covers EVERY moved row whose discrete decisions agree
+    # (at most 10 % of a phase's moved rows excluded, the fraction printed); on top, where the continuous inputs agree
     # too (f_n of the point and its update neighbours within 1e-6, input positions within 1e-7 x bbox, edge vector
-    # within 1e-6 rad); the injected variant feeds identical inputs everywhere
+    # within 1e-6 rad) the phase's own arithmetic is held to the single-step gate.  The injected variant feeds
+    # identical inputs everywhere.
     fn_tight = np.abs(got["f_n"] - ref_fn).max(1) < 1e-6
     edge_tight = angle(got["edge"], ref_edge) < 1e-6 if not injected else np.ones(len(ref_cls), bool)
     prev = [pos0] + list(ref_after)
-    stats = {}
+    stats, tstats = {}, {}
     for ph in range(3):
         dev_ = np.linalg.norm(got[f"pos_after_{ph}"] - ref_after[ph], axis=1) / bbox
         moved = ref_cls == ph
@@ -152,23 +154,33 @@ def check_stages(got, ref_cls, ref_fn, ref_eig2, ref_edge, ref_after, knn, pos0,
         tight = fn_tight & fn_tight[nb].all(1) & pos_tight & pos_tight[nb].all(1)
         if ph == 1:
             tight &= edge_tight
-        m = dec_ok & moved & (tight if not injected else True)
+        m = dec_ok & moved
         stats[ph] = (float(dev_[m].max()), float(np.percentile(dev_[m], 99)), float(np.percentile(dev_[m], 99.9)),
-                     float(1 - dec_ok[moved].mean()), float(1 - m.sum() / max(moved.sum(), 1)))
+                     float(1 - m.sum() / max(moved.sum(), 1)))
+        mt = m & tight
+        tstats[ph] = (float(dev_[mt].max()) if mt.any() else 0.0,
+                      float(np.percentile(dev_[mt], 99.9)) if mt.any() else 0.0,
+                      float(1 - mt.sum() / max(moved.sum(), 1)))
         if ph == 0:
             assert (dev_[dec_ok & ~moved] == 0).all(), (label, ph)   # the flat phase copies the others
     print(label, "excluded", round(float(excl), 5), "eig max", float(e.max()),
-          "phases (max, p99, p99.9, decisions differ, excluded)", stats)
+          "phases (max, p99, p99.9, excluded: decisions differ)", stats,
+          "tight-input rows (max, p99.9, excluded)", tstats)
     # SURVEY §8(c)'s single-step gate (identical inputs): <= 1e-6 x bbox, every phase.  The edge / feature / corner
     # steps restate the reference's inv_ex (MKL getrf(Aᵀ) + getrs('T'), bitwise:
     # test_capi.py::test_host_inv3_matches_torch_bitwise), its einsum products and its list-order sums; the flat step
     # differs only in the global centre's summation order (f64 here, a float32 torch mean there).
     # The chained variant's edge vectors come from NVT2's own solver (within 5e-7 / gap of LAPACK's,
     # test_nvt2_jacobi_matches_lapack_restatement) and move the edge step's x by up to |x| times that angle: its gate
-    # is 3e-6 x bbox, still two orders inside §8(c)'s one-iteration end-to-end gate (p99 3e-4 x bbox).
+    # over every decided row is p99 <= 2e-6 / p99.9 <= 3e-6 x bbox, two orders inside §8(c)'s one-iteration
+    # end-to-end gate; rows with tight inputs meet the single-step 1e-6 at p99.9.
     for ph in range(3):
-        assert stats[ph][2] <= (1e-6 if injected else 3e-6), (label, ph, stats[ph])
-        assert stats[ph][4] < (0.02 if injected else 0.8), (label, ph, stats[ph])
+        if injected:
+            assert stats[ph][2] <= 1e-6 and stats[ph][3] < 0.02, (label, ph, stats[ph])
+        else:
+            assert stats[ph][1] <= 2e-6 and stats[ph][2] <= 3e-6, (label, ph, stats[ph])
+            assert stats[ph][3] <= 0.10, (label, ph, stats[ph])
+            assert tstats[ph][1] <= 1e-6, (label, ph, tstats[ph])
     assert dec_ok.mean() > (0.99 if injected else 0.90), (label, dec_ok.mean())
     return stats
 

@@ -94,10 +94,11 @@ def _worker(rank, world, port, out_path, halo_scale, opts=None):
         pos, nrm = _cloud()
         params, _ = _params(pos)
         tr = TorchTransport()
-        sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, halo=_halo(pos, K) * halo_scale,
+        # only the coordinator (rank 0) hands in the cloud; the others receive their slab + halo from it
+        sd = SlabDenoiser(pos if rank == 0 else None, nrm if rank == 0 else None, max(K, KU), transport=tr, halo=_halo(pos, K) * halo_scale,
                           engine_factory=CpuSlabEngine, **opts)
         owned0 = sd.owned_global.numel()
-        halo0 = sd.plan.halo
+        halo0 = sd.halo
         if rebalance_after is None:
             sd.iterate(params, ITERS)
         else:
@@ -117,7 +118,7 @@ def _worker(rank, world, port, out_path, halo_scale, opts=None):
         dist.all_gather(allo, owned)
         if rank == 0:
             np.savez(out_path, pos=p.numpy(), n=n.numpy(), err=int(flag), halo=sd.halo_points, replans=sd.replans,
-                     final_halo=sd.plan.halo, halo0=halo0, owned=torch.stack(allo).numpy())
+                     final_halo=sd.halo, halo0=halo0, owned=torch.stack(allo).numpy())
     finally:
         dist.destroy_process_group()
 
@@ -215,3 +216,16 @@ def test_slab_world4_gloo_matches_oracle(tmp_path):
     bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
     np.testing.assert_allclose(res["pos"], rp, rtol=0, atol=1e-6 * bbox)
     np.testing.assert_allclose(res["n"], rn, rtol=0, atol=1e-5)
+
+
+def test_bench_refuses_more_gpus_than_the_box_has():
+    """`bench.py --gpus N` with fewer than N GPUs (none here) stops before any rank starts, unless told to rehearse
+    on one GPU."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("this box has the GPUs")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1"], cwd=root,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "needs 2 GPUs" in r.stderr

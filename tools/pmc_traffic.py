@@ -71,7 +71,12 @@ def main():
             for e in v:
                 if e.get("hbm_bytes_per_launch") is not None:
                     per_iter += e["hbm_bytes_per_launch"] * e["launches_fetch"] / n_iter
-    res = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, csv; "
+    # the build the counters measured (the in-tree libpcd.so, or PCD_LIB): the bench reads the file only when its own
+    # library has the same build id
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                    "normal-guided-pointcloud-denoiser_amd"))
+    import pcd_native
+    res = {"build_id": pcd_native.build_id(), "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, csv; "
                      "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch (gfx950 FETCH_SIZE counts half; x2 "
                      "calibrated for 4/8/16-B reads and 16-B gathers, profiles/r3/calib_traffic.json); L2-miss bytes "
                      "including Infinity-Cache hits (an upper bound on HBM bytes)",
