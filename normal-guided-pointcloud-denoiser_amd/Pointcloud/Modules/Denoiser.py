@@ -1,7 +1,10 @@
 """Class-specific position updates (drop-in for Pointcloud/Modules/Denoiser.py).
 
-Every step is one pcd_step_csr launch over the selection's segments: 3x3 accumulation in registers, LU solve with
-the reference's exact-zero-pivot mask (torch.linalg.inv_ex info), displacement clamp.  flat_step / new_step first
+Every step is one pcd_step_csr launch over the selection's segments: 3x3 accumulation in registers, then the
+reference's torch.linalg.inv_ex restated operation for operation (MKL getrf(Aᵀ) + getrs('T'), pcd_device.h inv3_ref)
+and its einsum-order product, with the exact-zero-pivot mask (inv_ex info) and the displacement clamp -- with the
+reference's own inputs injected the edge / feature / corner steps are bit-identical to it
+(tests/test_gpu_stages.py, test_capi.py::test_host_inv3_matches_torch_bitwise).  flat_step / new_step first
 reduce the GLOBAL centre and spread of all neighbour rows (Denoiser.py:106-107, :138) on the device.
 Reference lines: corner_step :26-51, edge_step :53-88, flat_step :90-119, new_step :121-172,
 feature_step :174-219, dummy_step :221-232.

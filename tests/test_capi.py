@@ -129,50 +129,27 @@ def test_host_solve3():
     np.testing.assert_allclose(x[good], xr, rtol=1e-4, atol=1e-4)
 
 
-def _inv_cases(rng, m):
-    """SPD systems shaped like feature_step's A (I + n nᵀ + Σ n_j n_jᵀ + k_u n nᵀ), edge_step-like sums of rank-2
-    terms, random Gaussian matrices, and exactly singular ones."""
-    u = lambda a: a / np.linalg.norm(a, axis=-1, keepdims=True)
-    n = u(rng.normal(size=(m, 3)))
-    nj = u(n[:, None, :] + 0.3 * rng.normal(size=(m, 8, 3)))
-    feat = np.eye(3)[None] + 9 * n[:, :, None] * n[:, None, :] + (nj[..., :, None] * nj[..., None, :]).sum(1)
-    y = u(rng.normal(size=(m, 3)))
-    p = nj - (nj * y[:, None]).sum(-1, keepdims=True) * y[:, None]
-    edge = (p[..., :, None] * p[..., None, :]).sum(1) + 8 * y[:, :, None] * y[:, None, :]
-    gauss = rng.normal(size=(m, 3, 3))
-    A = np.concatenate([feat, edge, gauss]).astype(np.float32)
-    A[:50, 2] = 0.0                                # exactly singular rows / columns
-    A[50:100, :, 1] = 0.0
-    A[100:150, 0] = A[100:150, 1]                  # equal rows
-    return A
-
-
-def test_host_inv3_matches_torch_bitwise():
+def test_host_inv3_matches_torch_bitwise(golden):
     """inv3_ref (pcd_device.h, what every position step runs) against torch.linalg.inv_ex -- the reference's own call
-    (Denoiser.py:43, 80, 163, 210) -- bit for bit, with the same info mask.  torch restates inv_ex as getrf(Aᵀ) +
-    getrs('T', I) through MKL; the fixtures were generated with this torch/MKL build."""
-    rng = np.random.default_rng(11)
-    A = _inv_cases(rng, 100_000)
-    inv, ok = nat.host_inv3(A)
-    ref, info = torch.linalg.inv_ex(torch.from_numpy(A))
-    ref, ok_ref = ref.numpy(), info.numpy() == 0
+    (Denoiser.py:43, 80, 163, 210) -- bit for bit, with the same info mask: torch's outputs saved by
+    tests/golden/make_inv_golden.py (torch restates inv_ex as getrf(Aᵀ) + getrs('T', I) through MKL, whose code path
+    depends on the CPU, so the reference values are data, not a live call)."""
+    g = golden("inv_ex")
+    inv, ok = nat.host_inv3(g["A"])
+    ok_ref = g["info"] == 0
     assert (ok == ok_ref).all()
     assert ok.mean() > 0.99
-    same = (inv.view(np.uint32) == ref.view(np.uint32)).all(axis=(1, 2))
+    same = (inv.view(np.uint32) == g["inv"].view(np.uint32)).all(axis=(1, 2))
     assert same[ok].all(), f"{(~same[ok]).sum()} of {ok.sum()} inverses differ"
 
 
-def test_host_solve3_is_inverse_then_product():
-    """solve3 = einsum("nij,nj->ni", inv_ex(A), b) as torch computes it (row sums (a0 b0 + a1 b1) + a2 b2)."""
-    rng = np.random.default_rng(12)
-    A = _inv_cases(rng, 20_000)
-    b = rng.normal(size=(A.shape[0], 3)).astype(np.float32) * 10
-    x, ok = nat.host_solve3(A, b)
-    inv, info = torch.linalg.inv_ex(torch.from_numpy(A))
-    ref = torch.einsum("nij,nj->ni", inv, torch.from_numpy(b)).numpy()
-    ok_ref = info.numpy() == 0
-    assert (ok == ok_ref).all()
-    np.testing.assert_array_equal(x[ok], ref[ok])
+def test_host_solve3_is_inverse_then_product(golden):
+    """solve3 = einsum("nij,nj->ni", inv_ex(A), b) as torch computes it (row sums (a0 b0 + a1 b1) + a2 b2), against
+    torch's saved outputs."""
+    g = golden("inv_ex")
+    x, ok = nat.host_solve3(g["A"], g["b"])
+    assert (ok == (g["info"] == 0)).all()
+    np.testing.assert_array_equal(x[ok], g["x"][ok])
 
 
 def test_orientation_host_matches_oracle(golden):

@@ -234,20 +234,15 @@ def test_cpsd_driver_oracle_matches_reference(golden):
             assert np.median(dev) < 1e-5 and np.percentile(dev, 99) < 5e-3, np.percentile(dev, 99)
 
 
-def test_oracle_inv_ex_is_torchs_bitwise():
-    """The oracle's numpy restatement of torch.linalg.inv_ex (getrf(A^T) + getrs('T') in MKL's AVX-512 arithmetic) is
-    torch's own result bit for bit on this container's CPU, where the fixtures were generated (random, SPD-like and
-    singular 3x3 systems)."""
-    import torch
-    rng = np.random.default_rng(21)
-    u = lambda a: a / np.linalg.norm(a, axis=-1, keepdims=True)
-    n = u(rng.normal(size=(50000, 3)))
-    nj = u(n[:, None, :] + 0.3 * rng.normal(size=(50000, 8, 3)))
-    A = np.concatenate([np.eye(3)[None] + 9 * n[:, :, None] * n[:, None, :] + (nj[..., :, None] * nj[..., None, :]).sum(1),
-                        rng.normal(size=(50000, 3, 3))]).astype(np.float32)
-    A[:20, 1] = 0.0
-    inv, ok = O.inv_ex(A)
-    ref, info = torch.linalg.inv_ex(torch.from_numpy(A))
-    ref = ref.numpy()
-    assert (ok == (info.numpy() == 0)).all()
-    np.testing.assert_array_equal(inv[ok], ref[ok])
+def test_oracle_inv_ex_is_torchs_bitwise(golden):
+    """The oracle's numpy restatements of torch.linalg.inv_ex (getrf(A^T) + getrs('T') in MKL's AVX-512 arithmetic) and
+    of torch's CPU einsum are torch's own results bit for bit: saved torch outputs (tests/golden/make_inv_golden.py,
+    random, SPD-like and singular 3x3 systems), so the check does not depend on this host's MKL code path."""
+    g = golden("inv_ex")
+    inv, ok = O.inv_ex(g["A"])
+    assert (ok == (g["info"] == 0)).all()
+    np.testing.assert_array_equal(inv[ok], g["inv"][ok])
+    x = O._einsum("nij,nj->ni", g["inv"], g["b"])
+    np.testing.assert_array_equal(x, g["x"])
+    np.testing.assert_array_equal(O._einsum("nkij,nkj->nki", g["M4"], g["v4"]), g["y4"])
+    np.testing.assert_array_equal(O._einsum("nkij,nj->nki", g["M4"], g["v4"][:, 0]), g["y5"])
