@@ -26,7 +26,6 @@
 #include "pcd_lists.h"
 #include "pcd_ops.h"
 #include "pcd_qknn.h"
-#include "pcd_dense.h"
 
 namespace pcd {
 int knn_cap(int k);
@@ -1216,12 +1215,6 @@ static int select_rows(pcd_denoiser* dn, const RowMap& rm, int32_t* list, unsign
 #ifndef PCD_REDO_COMPACT
 #define PCD_REDO_COMPACT 1   // the redo list by k_compact_fail (one atomic per 4,096 rows); 0: rocprim::select (row order)
 #endif
-#ifndef PCD_DENSE_TILE
-#define PCD_DENSE_TILE 1     // dense first anchoring by cell tiles (pcd_dense.h) when every row is active
-#endif
-#ifndef PCD_TILE_GRID
-#define PCD_TILE_GRID 65536  // waves (one per brick, grid-stride past this)
-#endif
 #ifndef PCD_NVT1_OVERLAP
 #define PCD_NVT1_OVERLAP 0   // measured: the side-stream NVT1 slows the re-anchoring more than it hides
 #endif
@@ -1253,7 +1246,6 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     const dim3 grd_rq((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), dense ? 16384 : PCD_RQ_GRID));
     const dim3 grd_wave((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), PCD_REDO_GRID));
     const dim3 grd_dq((unsigned)std::min<int64_t>(cdiv(rm.nq, 4 * std::max(PCD_DENSE_Q, 1)), 16384));
-    const dim3 grd_tile((unsigned)std::max<int64_t>(std::min<int64_t>(dn->g->bricks, PCD_TILE_GRID), 1));
     const dim3 grd_anc((unsigned)cdiv(rm.nq, kAnchorBS)), grd_cmp((unsigned)cdiv(rm.nq, kCompactBS * kCompactPer));
     int rc = PCD_OK;
     // Dense (no anchors): every row is re-anchored, then NVT1 runs over all rows.  Seeded: the anchor test, then
@@ -1273,10 +1265,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     case C:                                                                                                            \
         if (dense) {                                                                                                   \
             if (ev) PCD_HIP(hipEventRecord(ev[1], st));                                                                \
-            if (PCD_DENSE_TILE && !rm.rows)                                                                            \
-                hipLaunchKernelGGL((k_knn_dense_tile<2 * C>), grd_tile, dim3(64), 0, st, gv, P, N, dn->g->bricks,      \
-                                   kstore, PCD_RQ_RDENSE, dn->anc, dn->alist, dn->idx, dn->spill, spill_cnt);          \
-            else if (PCD_DENSE_Q > 0)                                                                                  \
+            if (PCD_DENSE_Q > 0)                                                                                       \
                 hipLaunchKernelGGL((k_knn_dense_q<2 * C, (PCD_DENSE_Q > 0 ? PCD_DENSE_Q : 1)>), grd_dq, blk, 0, st, gv, P, N, rm, \
                                    kstore, PCD_RQ_RDENSE, dn->anc, dn->alist, dn->idx, dn->spill, spill_cnt);          \
             else                                                                                                       \
