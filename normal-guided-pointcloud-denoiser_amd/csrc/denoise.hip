@@ -1632,6 +1632,9 @@ int pcd_denoiser_check(pcd_denoiser* dn, void* stream) {
 
 int pcd_denoiser_status(pcd_denoiser* dn, int* bits, void* stream) {
     PCD_CHECK_ARG(dn && bits, "null argument");
+    // (an exchange still in flight finishes first: a collective the caller issues next on its comm -- the slab
+    // driver's coverage verdict -- then follows it in stream order rather than racing it on another stream)
+    if (settle(dn, as_stream(stream)) != PCD_OK) return PCD_ERR_HIP;
     PCD_HIP(hipMemcpyAsync(bits, dn->err, sizeof(int), hipMemcpyDeviceToHost, as_stream(stream)));
     PCD_HIP(hipStreamSynchronize(as_stream(stream)));
     return PCD_OK;
