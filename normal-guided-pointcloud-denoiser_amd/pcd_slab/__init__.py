@@ -716,3 +716,175 @@ def gather_global(state, n_total: int, transport) -> tuple:
         out_p[gi] = b[:, 1:4].float()
         out_n[gi] = b[:, 4:7].float()
     return out_p, out_n
+
+
+# ----------------------------------------------------------------------------------------------- mesh update
+class HipMeshEngine:
+    """Mesh.updateVertices' Jacobi sweep (pcd_mesh_update / pcd_mesh_update_f32) over one rank's local mesh: the
+    faces incident to its own vertices (ascending global face id) and every vertex of those faces."""
+
+    def __init__(self, v, f, fn, fp32=True):
+        dev = nat.device()
+        self.fp32 = bool(fp32)
+        dt, it = (torch.float32, torch.int32) if fp32 else (torch.float64, torch.int64)
+        self.v = v.to(dev, dt).contiguous()
+        self.f = f.to(dev, it).contiguous()
+        self.fn = fn.to(dev, dt).contiguous()
+        self.vf, self.ni = nat.mesh_vta(self.f, self.v.size(0), out_dtype=it)
+
+    def sweep(self):
+        (nat.mesh_update_f32 if self.fp32 else nat.mesh_update)(self.v, self.f, self.fn, self.vf, self.ni, 1)
+
+
+class MeshSlabs:
+    """Mesh.updateVertices (PatchGeneration/Modules/Mesh.py:377-418) over vertex slabs, one rank per GPU (SURVEY.md
+    §8(e): the mesh update shards by vertex ownership).
+
+    Rank 0, the coordinator, holds the mesh (v [nv, 3], f [nf, 3], face normals fn [nf, 3]; the other ranks pass None)
+    and cuts the vertices into slabs of equal count along the longest bbox axis.  Rank r owns the vertices of slab r;
+    its local mesh is every face incident to an owned vertex (in ascending global face id, so each vertex sums its
+    faces in the reference's order) and every vertex of those faces -- the owned ones plus a one-ring halo.  A sweep
+    is the Jacobi update of the local mesh, then the halo rows are refreshed from their owners (point-to-point to the
+    slab neighbours).  An owned vertex sees all of its faces and the previous sweep's positions of their corners, so
+    the owned rows equal the one-GPU sweep bit for bit (fp64 and fp32).  engine_factory(v, f, fn) -> an object with
+    `v` (local rows, updated in place) and `sweep()`: the HIP engine by default (the CPU tests use the oracle's)."""
+
+    def __init__(self, v, f, fn, transport=None, fp32=True, engine_factory=None, native=None):
+        self.t = transport or LocalTransport()
+        rank, world = self.t.rank, self.t.world
+        self.native = (engine_factory is None) if native is None else bool(native)
+        self.comm = self.t.native_comm() if (self.native and world > 1) else None
+        dev = nat.device() if engine_factory is None else torch.device("cpu")
+        self.dev = dev
+        share = None
+        if rank == 0:
+            v, f, fn = torch.as_tensor(v), torch.as_tensor(f).long(), torch.as_tensor(fn)
+            nv = v.size(0)
+            assert world >= 1 and nv >= world, "need at least one vertex per rank"
+            vd = v.to(dev)
+            axis = int(torch.argmax(vd.max(0).values - vd.min(0).values))
+            order = torch.sort(vd[:, axis].contiguous(), stable=True).indices
+            owner = torch.empty(nv, dtype=torch.int64, device=dev)
+            for r in range(world):
+                owner[order[(r * nv) // world:((r + 1) * nv) // world]] = r
+            fdev, fndev = f.to(dev), fn.to(dev)
+            fown = owner[fdev]                                           # [nf, 3]
+            shares = []
+            for r in range(world):
+                faces = torch.nonzero((fown == r).any(1)).flatten()      # ascending global face id
+                # ascending global vertex id: the corners of those faces and every owned vertex (an isolated one has
+                # no face: degree 0, the reference's 0 / 0)
+                lverts = torch.unique(torch.cat([fdev[faces].flatten(), torch.nonzero(owner == r).flatten()]))
+                to_local = torch.full((nv,), -1, dtype=torch.int64, device=dev)
+                to_local[lverts] = torch.arange(lverts.numel(), device=dev)
+                shares.append((lverts, faces, to_local))
+            self.owner, self.n_total = owner, nv
+            for r in range(world):
+                lverts, faces, to_local = shares[r]
+                peers, send_l, recv_l = [], [], []
+                for q in range(world):
+                    if q == r:
+                        continue
+                    lq = shares[q][0]
+                    out = lq[owner[lq] == r]                             # mine, held by q
+                    inc = lverts[owner[lverts] == q]                     # q's, held by me
+                    if out.numel() or inc.numel():
+                        peers.append(q)
+                        send_l.append(to_local[out])
+                        recv_l.append(to_local[inc])
+                pkg = (lverts, torch.nonzero(owner[lverts] == r).flatten(), to_local[fdev[faces]],
+                       vd[lverts], fndev[faces], peers, send_l, recv_l)
+                if r == 0:
+                    share = pkg
+                else:
+                    self._send_pkg(pkg, r)
+        else:
+            share = self._recv_pkg()
+            self.owner, self.n_total = None, None
+        lverts, owned, lf, lv, lfn, self.peers, self.send_local, self.recv_local = share
+        self.local, self.owned_local = lverts, owned
+        self.owned_global = lverts[owned]
+        if self.n_total is None:
+            self.n_total = -1
+        self.e = (engine_factory or (lambda a, b, c: HipMeshEngine(a, b, c, fp32)))(lv, lf, lfn)
+        self.halo_rows = sum(int(x.numel()) for x in self.recv_local)
+
+    # -- coordinator -> rank (the mesh share), as pcd_slab.SlabDenoiser hands out its slabs
+    def _p2p_send(self, t, dst):
+        if self.comm is not None:
+            self.comm.sendrecv(dst, t.contiguous().to(nat.device()), -1, None)
+        else:
+            self.t.send(t, dst)
+
+    def _p2p_recv(self, shape, dtype, src):
+        if self.comm is not None:
+            return self.comm.sendrecv(-1, None, src, torch.empty(shape, dtype=dtype, device=nat.device()))
+        return self.t.recv(torch.empty(shape, dtype=dtype, device=self.dev), src)
+
+    def _send_pkg(self, pkg, dst):
+        lverts, owned, lf, lv, lfn, peers, send_l, recv_l = pkg
+        ints = torch.cat([x.to(self.dev, torch.int64).flatten() for x in
+                          [lverts, owned, lf, torch.tensor(peers, dtype=torch.int64),
+                           torch.tensor([x.numel() for x in send_l], dtype=torch.int64),
+                           torch.tensor([x.numel() for x in recv_l], dtype=torch.int64)] + send_l + recv_l])
+        rows = torch.cat([lv.to(self.dev, torch.float64).flatten(), lfn.to(self.dev, torch.float64).flatten()])
+        head = torch.tensor([lverts.numel(), owned.numel(), lf.size(0), len(peers), ints.numel(), rows.numel(), 0, 0],
+                            dtype=torch.int64)
+        for t in (head, ints, rows):
+            self._p2p_send(t, dst)
+
+    def _recv_pkg(self):
+        nl, no, nf, npeers, nints, nrows = self._p2p_recv((8,), torch.int64, 0).cpu().tolist()[:6]
+        ints = self._p2p_recv((nints,), torch.int64, 0).to(self.dev)
+        rows = self._p2p_recv((nrows,), torch.float64, 0).to(self.dev)
+        o = 0
+        lverts, o = ints[o:o + nl], o + nl
+        owned, o = ints[o:o + no], o + no
+        lf, o = ints[o:o + 3 * nf].view(nf, 3), o + 3 * nf
+        peers, o = ints[o:o + npeers].tolist(), o + npeers
+        ns, o = ints[o:o + npeers].tolist(), o + npeers
+        nr, o = ints[o:o + npeers].tolist(), o + npeers
+        send_l, recv_l = [], []
+        for c in ns:
+            send_l.append(ints[o:o + c])
+            o += c
+        for c in nr:
+            recv_l.append(ints[o:o + c])
+            o += c
+        lv, lfn = rows[:3 * nl].view(nl, 3), rows[3 * nl:].view(nf, 3)
+        return lverts, owned, lf, lv, lfn, peers, send_l, recv_l
+
+    # -- sweeps
+    def _exchange(self):
+        """Halo rows from their owners, peer by peer in ascending rank (no cycle of blocking pairs)."""
+        v = self.e.v
+        for q, peer in enumerate(self.peers):
+            out = v[self.send_local[q].to(v.device)].contiguous()
+            inc = torch.empty((self.recv_local[q].numel(), 3), dtype=v.dtype, device=v.device)
+            if self.comm is not None:
+                self.comm.sendrecv(peer if out.numel() else -1, out if out.numel() else None,
+                                   peer if inc.numel() else -1, inc if inc.numel() else None)
+            else:
+                dist = self.t.dist
+                ops = []
+                hi = torch.empty(inc.shape, dtype=inc.dtype)
+                if inc.numel():
+                    ops.append(dist.P2POp(dist.irecv, hi, peer, self.t.group))
+                if out.numel():
+                    ops.append(dist.P2POp(dist.isend, out.cpu(), peer, self.t.group))
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+                inc = hi.to(v.device)
+            if inc.numel():
+                v[self.recv_local[q].to(v.device)] = inc
+
+    def update(self, k=15):
+        """k Jacobi sweeps (Mesh.updateVertices' loop), each followed by the halo refresh."""
+        for _ in range(int(k)):
+            self.e.sweep()
+            if self.t.world > 1:
+                self._exchange()
+
+    def owned_state(self):
+        """(global vertex ids, positions) of this rank's own vertices."""
+        return self.owned_global, self.e.v[self.owned_local.to(self.e.v.device)]

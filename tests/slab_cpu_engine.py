@@ -129,3 +129,15 @@ class CpuSlabEngine:
 
     def store(self):
         return torch.from_numpy(self.pos.copy()), torch.from_numpy(self.nrm.copy())
+
+
+class CpuMeshEngine:
+    """Mesh.updateVertices' Jacobi sweep on one rank's local mesh by the oracle (float64), for pcd_slab.MeshSlabs."""
+
+    def __init__(self, v, f, fn):
+        self.v = torch.as_tensor(v, dtype=torch.float64).clone()
+        self.f = np.asarray(f, np.int64)
+        self.fn = np.asarray(fn, np.float64)
+
+    def sweep(self):
+        self.v = torch.from_numpy(O.mesh_update(self.v.numpy(), self.f, self.fn, k=1))

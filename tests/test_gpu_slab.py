@@ -376,3 +376,60 @@ def test_bench_gpus2_self_launch_rehearsal():
     assert line["slab"]["world"] == 2 and line["slab"]["transport"] == "host"
     assert sum(line["slab"]["owned_rows"]) == 800_000 and min(line["slab"]["halo_rows"]) > 0
     assert line["n1"]["points"] == 400_000 and line["value"] > 0
+
+
+def _mesh_inputs():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    m = np.load(os.path.join(root, "data", "stanford_bunny_mesh.npz"))
+    v, f = m["v"].astype(np.float64), m["f"].astype(np.int64)
+    cr = np.cross(v[f[:, 1]] - v[f[:, 0]], v[f[:, 2]] - v[f[:, 1]])
+    fn = cr / np.maximum(np.linalg.norm(cr, axis=1, keepdims=True), 1e-30)
+    fn = fn + 0.2 * np.random.default_rng(4).standard_normal(fn.shape)
+    return v, f, fn / np.linalg.norm(fn, axis=1, keepdims=True)
+
+
+def _mesh_one_gpu(v, f, fn, k, fp32, dev):
+    dt, it = (torch.float32, torch.int32) if fp32 else (torch.float64, torch.int64)
+    vd = torch.from_numpy(v).to(dev, dt).contiguous()
+    fd = torch.from_numpy(f).to(dev, it).contiguous()
+    nd = torch.from_numpy(fn).to(dev, dt).contiguous()
+    vf, ni = nat.mesh_vta(fd, vd.size(0), out_dtype=it)
+    (nat.mesh_update_f32 if fp32 else nat.mesh_update)(vd, fd, nd, vf, ni, k)
+    return vd.cpu().numpy()
+
+
+def _mesh_worker_gpu(rank, world, port, prefix, k, fp32):
+    import torch.distributed as dist
+    from pcd_slab import MeshSlabs
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        v, f, fn = _mesh_inputs() if rank == 0 else (None, None, None)
+        ms = MeshSlabs(v, f, fn, transport=TorchTransport(), fp32=fp32)
+        ms.update(k)
+        ids, pv = ms.owned_state()
+        np.savez(f"{prefix}_{rank}.npz", ids=ids.cpu().numpy(), v=pv.cpu().numpy(), halo=ms.halo_rows)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fp32", [False, True], ids=["fp64", "fp32"])
+def test_mesh_slabs_world2_equal_one_gpu(gpu, tmp_path, fp32):
+    """Mesh.updateVertices over two vertex slabs (pcd_slab.MeshSlabs: the HIP sweep on each rank's local mesh, the
+    one-ring halo refreshed through libpcd's communicator -- here its host transport, both ranks on the box's GPU)
+    against the one-GPU kernel: every vertex bit-identical after 5 sweeps, in fp64 and in fp32."""
+    import torch.multiprocessing as mp
+    k = 5
+    prefix = str(tmp_path / ("m32" if fp32 else "m64"))
+    mp.spawn(_mesh_worker_gpu, args=(2, _free_port(), prefix, k, fp32), nprocs=2, join=True)
+    v, f, fn = _mesh_inputs()
+    ref = _mesh_one_gpu(v, f, fn, k, fp32, gpu)
+    got = np.full_like(ref, np.nan)
+    for r in range(2):
+        z = np.load(f"{prefix}_{r}.npz")
+        assert int(z["halo"]) > 0
+        got[z["ids"]] = z["v"]
+    np.testing.assert_array_equal(got, ref)

@@ -229,3 +229,53 @@ def test_bench_refuses_more_gpus_than_the_box_has():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1"], cwd=root,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "needs 2 GPUs" in r.stderr
+
+
+def _bunny_mesh():
+    m = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data",
+                             "stanford_bunny_mesh.npz"))
+    v, f = m["v"].astype(np.float64), m["f"].astype(np.int64)
+    cr = np.cross(v[f[:, 1]] - v[f[:, 0]], v[f[:, 2]] - v[f[:, 1]])
+    fn = cr / np.maximum(np.linalg.norm(cr, axis=1, keepdims=True), 1e-30)
+    # a perturbed field of target normals, so the sweeps move the vertices
+    rng = np.random.default_rng(4)
+    fn = fn + 0.2 * rng.standard_normal(fn.shape)
+    return v, f, fn / np.linalg.norm(fn, axis=1, keepdims=True)
+
+
+def _mesh_worker(rank, world, port, out_path, sweeps):
+    import torch.distributed as dist
+    from pcd_slab import MeshSlabs
+    from slab_cpu_engine import CpuMeshEngine
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        v, f, fn = _bunny_mesh() if rank == 0 else (None, None, None)
+        ms = MeshSlabs(v, f, fn, transport=TorchTransport(), engine_factory=CpuMeshEngine)
+        ms.update(sweeps)
+        ids, pv = ms.owned_state()
+        np.savez(f"{out_path}_{rank}.npz", ids=ids.numpy(), v=pv.numpy(), halo=ms.halo_rows)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_mesh_slabs_match_one_process_bitwise(tmp_path, world):
+    """Mesh.updateVertices over vertex slabs (pcd_slab.MeshSlabs): gloo ranks, the oracle's sweep as the
+    engine, every owned vertex equal to the single-process oracle bit for bit after 3 sweeps -- each owned vertex
+    sums all of its faces in the reference's order and reads the previous sweep's halo rows."""
+    import torch.multiprocessing as mp
+    sweeps = 3
+    prefix = str(tmp_path / f"mesh{world}")
+    mp.spawn(_mesh_worker, args=(world, _free_port(), prefix, sweeps), nprocs=world, join=True)
+    v, f, fn = _bunny_mesh()
+    ref = O.mesh_update(v, f, fn, k=sweeps)
+    got = np.full_like(ref, np.nan)
+    halos = []
+    for r in range(world):
+        z = np.load(f"{prefix}_{r}.npz")
+        got[z["ids"]] = z["v"]
+        halos.append(int(z["halo"]))
+    assert min(halos) > 0
+    np.testing.assert_array_equal(got, ref)
