@@ -694,6 +694,9 @@ def main():
         out["cpu_baseline"], out["parity"] = cpu_baseline(args.k, args.k_update, args.cpu_sample, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if mode == "slab":
+        del sd
+        tr.close()             # libpcd's RCCL communicator, torn down by every rank at this point
     if dist:
         dist.destroy_process_group()
 

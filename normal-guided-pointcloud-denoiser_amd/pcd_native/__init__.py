@@ -562,11 +562,15 @@ class Comm:
               "pcd_allreduce_scalars")
         return t
 
-    def __del__(self):
+    def destroy(self):
+        """pcd_comm_destroy now (every rank at the same point of its program: the RCCL communicator's teardown)."""
         h = getattr(self, "handle", None)
         if h is not None and h.value and _lib is not None:
             _lib.pcd_comm_destroy(h)
-            self.handle = None
+        self.handle = None
+
+    def __del__(self):
+        self.destroy()
 
 
 def make_cpsd_params(r, d, rho=0.9, tau=0.3, damp=3.0, step_clamp=None, alphas=(0.1, 1.0, 1.0), k_update=8):

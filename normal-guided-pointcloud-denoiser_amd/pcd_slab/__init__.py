@@ -181,6 +181,15 @@ class TorchTransport:
         self._comm = nat.Comm.host(self.world, self.rank, exchange, allreduce)
         return self._comm
 
+    def close(self):
+        """Tear libpcd's communicator down (collective in spirit: every rank calls it at the same point, after its
+        last use -- drivers and engines holding it must be gone or done)."""
+        if self._comm is not None:
+            torch.cuda.synchronize()
+            self._comm.destroy()
+            self._comm = None
+        self.dist.barrier(self.group)
+
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         h = t.cpu() if t.device.type != "cpu" else t
         self.dist.broadcast(h, src, self.group)
