@@ -18,6 +18,17 @@ for p in (PKG, ROOT):
         sys.path.insert(0, p)
 
 
+class ParityReport(UserWarning):
+    """A measured parity figure (deviation percentiles, excluded fractions): issued as a warning so that it shows in
+    pytest's warnings summary even for passing tests under -q (the round-end GPU run), and printed for -s."""
+
+
+def report(msg: str):
+    import warnings
+    print(msg)
+    warnings.warn(msg, ParityReport, stacklevel=2)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); run with -m gpu")
 

@@ -14,6 +14,7 @@ import torch
 from oracle import pcd_oracle as O
 from Pointcloud.Modules.Object import Pointcloud
 from Pointcloud.Modules.Processor import Processor
+from conftest import report
 
 pytestmark = pytest.mark.gpu
 
@@ -153,7 +154,7 @@ def test_cpsd_driver_matches_reference(cpsd, gpu):
         proc = Processor(Pointcloud(v, T(n0, gpu).clone()))
         proc.cpsdDenoise(iterations=it, d=d)                         # original_pos = the call's input, as the ipynb
         dev = np.linalg.norm(v.cpu().numpy() - ref, axis=1) / bbox
-        print(f"cpsd driver it{it}: exact {np.mean(dev == 0):.4f} median {np.median(dev):.3g} "
+        report(f"cpsd driver it{it}: exact {np.mean(dev == 0):.4f} median {np.median(dev):.3g} "
               f"p99 {np.percentile(dev, 99):.3g} max {dev.max():.3g}")
         if it == 1:
             # the CPSD path's f32 eigen-solves (normal-filtered NVT / PVT, LAPACK-restated vs MKL ssyevd) differ from
@@ -206,7 +207,7 @@ def test_cpsd_fused_equals_op_by_op(cpsd, gpu, rscale):
             proc.cpsdDenoise(iterations=2, d=d, fused=False)
             out[fused] = proc.graph.pos.cpu().numpy()
     dev = np.linalg.norm(out[True] - out[False], axis=1) / bbox
-    print(f"rscale {rscale}: exact {np.mean(dev == 0):.4f} p99.9 {np.percentile(dev, 99.9):.3g} max {dev.max():.3g}")
+    report(f"rscale {rscale}: exact {np.mean(dev == 0):.4f} p99.9 {np.percentile(dev, 99.9):.3g} max {dev.max():.3g}")
     assert np.percentile(dev, 99.9) <= 1e-6 and np.median(dev) <= 1e-7, (np.percentile(dev, 99.9), np.median(dev))
 
 
@@ -237,5 +238,5 @@ def test_cpsd_fused_equals_op_by_op_large_cloud(gpu, rscale):
             proc.cpsdDenoise(iterations=1, d=d, fused=False)
             out[fused] = proc.graph.pos.cpu().numpy()
     dev = np.linalg.norm(out[True] - out[False], axis=1) / bbox
-    print(f"large rscale {rscale}: exact {np.mean(dev == 0):.4f} p99.9 {np.percentile(dev, 99.9):.3g} max {dev.max():.3g}")
+    report(f"large rscale {rscale}: exact {np.mean(dev == 0):.4f} p99.9 {np.percentile(dev, 99.9):.3g} max {dev.max():.3g}")
     assert np.percentile(dev, 99.9) <= 1e-6 and np.median(dev) <= 1e-7, (np.percentile(dev, 99.9), np.median(dev))

@@ -20,6 +20,7 @@ from Pointcloud.Modules.Processor import Processor
 from Pointcloud.Modules.Selector import Selection, Selector
 from Pointcloud.Modules.Utils import TorchUtils
 from PatchGeneration.Modules.Mesh import Mesh
+from conftest import report
 
 pytestmark = pytest.mark.gpu
 ANGLE = math.pi * 5 / 12
@@ -301,7 +302,7 @@ def test_fused_iteration_matches_reference(fan, gpu):
     assert np.percentile(a, 99) < 1e-4 and (a < 1e-2).mean() > 0.998
     bbox = np.linalg.norm(fan["pos0"].max(0) - fan["pos0"].min(0))
     dev = np.linalg.norm(pos - fan["it1_pos_after_2"], axis=1) / bbox
-    print(f"fandisk 1 iteration: median {np.median(dev):.3g} p99 {np.percentile(dev, 99):.3g} max {dev.max():.3g}")
+    report(f"fandisk 1 iteration: median {np.median(dev):.3g} p99 {np.percentile(dev, 99):.3g} max {dev.max():.3g}")
     assert np.percentile(dev, 99) <= 1e-5 and np.median(dev) <= 1e-7
 
 
@@ -476,7 +477,7 @@ def test_thesis_driver_matches_reference(golden, gpu):
     proc.thesisDenoise(iterations=1, d=float(g["d"]))
     bbox = np.linalg.norm(g["pos0"].max(0) - g["pos0"].min(0))
     dev1 = np.linalg.norm(v.cpu().numpy() - g["pos_it1"], axis=1) / bbox
-    print(f"thesis 1 iteration: median {np.median(dev1):.3g} p99 {np.percentile(dev1, 99):.3g} max {dev1.max():.3g}")
+    report(f"thesis 1 iteration: median {np.median(dev1):.3g} p99 {np.percentile(dev1, 99):.3g} max {dev1.max():.3g}")
     # (r5b: median 0, p99 1.9e-4, max 5.9e-3 x bbox: the thesis cloud's few discrete decisions -- classes, the
     # per-step clamp -- that round differently; the NVT path's own one-iteration gate is test_fused_iteration_matches_
     # reference's 1e-5)

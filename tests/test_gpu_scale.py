@@ -22,6 +22,7 @@ import pcd_native as nat
 from oracle import pcd_oracle as O
 from Pointcloud.Modules.Object import Pointcloud, sample_surface
 from Pointcloud.Modules.Processor import Processor
+from conftest import report
 
 pytestmark = pytest.mark.gpu
 
@@ -121,7 +122,7 @@ def _one_iteration_vs_oracle(pos, nrm, k, dev):
     agree = float((gc.cpu().numpy() == rcls).mean())
     bbox = float(np.linalg.norm(p0.max(0) - p0.min(0)))
     dev_pos = np.linalg.norm(gp.cpu().numpy() - rpos, axis=1) / bbox
-    print(f"{N} points, 1 iteration vs the oracle: classes {agree:.6f} median {np.median(dev_pos):.3g} "
+    report(f"{N} points, 1 iteration vs the oracle: classes {agree:.6f} median {np.median(dev_pos):.3g} "
           f"p99 {np.percentile(dev_pos, 99):.3g} p99.9 {np.percentile(dev_pos, 99.9):.3g} max {dev_pos.max():.3g}")
     assert agree >= 0.998, agree
     assert np.percentile(dev_pos, 99) <= 1e-5 and np.median(dev_pos) <= 1e-7, (np.percentile(dev_pos, 99),

@@ -26,6 +26,7 @@ import torch
 
 import pcd_native as nat
 from oracle import pcd_oracle as O
+from conftest import report
 
 pytestmark = pytest.mark.gpu
 K, KU = 32, 8
@@ -163,9 +164,9 @@ def check_stages(got, ref_cls, ref_fn, ref_eig2, ref_edge, ref_after, knn, pos0,
                       float(1 - mt.sum() / max(moved.sum(), 1)))
         if ph == 0:
             assert (dev_[dec_ok & ~moved] == 0).all(), (label, ph)   # the flat phase copies the others
-    print(label, "excluded", round(float(excl), 5), "eig max", float(e.max()),
-          "phases (max, p99, p99.9, excluded: decisions differ)", stats,
-          "tight-input rows (max, p99.9, excluded)", tstats)
+    report(f"{label} ({'injected' if injected else 'chained'}): NVT2 neighbourhoods excluded {float(excl):.5f}, eig max "
+           f"{float(e.max()):.3g}; phases (max, p99, p99.9, excluded: decisions differ) {stats}; tight-input rows (max, "
+           f"p99.9, excluded) {tstats}")
     # SURVEY §8(c)'s single-step gate (identical inputs): <= 1e-6 x bbox, every phase.  The edge / feature / corner
     # steps restate the reference's inv_ex (MKL getrf(Aᵀ) + getrs('T'), bitwise:
     # test_capi.py::test_host_inv3_matches_torch_bitwise), its einsum products and its list-order sums; the flat step
