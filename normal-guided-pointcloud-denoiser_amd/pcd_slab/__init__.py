@@ -374,7 +374,8 @@ class SlabDenoiser:
     the halo, cuts the slabs, and hands every rank its share -- slab + halo rows of the frozen snapshot, owned rows,
     routes -- over libpcd's communicator (pcd_comm_sendrecv: RCCL over xGMI in the product path).  No other rank ever
     holds or plans over the whole cloud.  A re-plan (thin halo, rebalance) gathers the owned state to rank 0, which
-    cuts again and hands out the new shares.  halo: slab widening in snapshot units (None: default_halo, on rank 0).
+    cuts again and hands out the new shares.  halo: slab widening in snapshot units (None: cut_halo, on rank 0 --
+    the snapshot's own largest k-ball reach past a face, x 1.25).
     check_every: iterations between coverage checks (0: never -- check() raises at the caller's request instead);
     halo_growth / max_replans: the thin-halo recovery."""
 
@@ -396,7 +397,7 @@ class SlabDenoiser:
             self.snap_pos, self.snap_n = snap_pos.detach().contiguous(), snap_n.detach().contiguous()
             self.dev = self.snap_pos.device
             if halo is None:
-                halo = default_halo(self.snap_pos, k_max)
+                halo = cut_halo(self.snap_pos, world, k_max) if world > 1 else 0.0
             self._lattice = (nat.grid_params(self.snap_pos.to(nat.device()), k_hint=self.k_hint)
                              if engine_factory is None else ([0.0, 0.0, 0.0], 0.0))
             plan = SlabPlan.build(self.snap_pos, world, halo, weights=weights)
@@ -683,6 +684,48 @@ class SlabDenoiser:
         pos, n = self.e.store()
         idx = self.owned_local.to(pos.device)
         return self.owned_global, pos[idx], n[idx]
+
+
+def cut_halo(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, axis: int | None = None) -> float:
+    """The halo the equal-count cut into `world` slabs needs at the snapshot, times `margin` for the drift of later
+    iterations: every snapshot point's k-ball (radius d_k, its k-th neighbour distance) must lie inside its slab
+    widened by the halo on the cut axis, so the halo is the largest reach of a ball past its slab's faces,
+    max_q (q + d_k(q) - hi_r, lo_r - q + d_k(q)) over the points near a face.  The balls that reach farthest belong
+    to the sparsest points near a cut (noise outliers), which default_halo's sample maximum prices everywhere three
+    times over.  Only the points within default_halo of a face are searched.  The coverage check still reports any
+    later ball that leaves the halo (a re-plan widens it)."""
+    dev = nat.device()
+    pos = snap_pos.to(dev)
+    n = pos.size(0)
+    if world == 1:
+        return 0.0
+    if axis is None:
+        axis = int(torch.argmax(pos.max(0).values - pos.min(0).values))
+    key = pos[:, axis].contiguous()
+    order = torch.sort(key, stable=True).indices
+    bounds = [(r * n) // world for r in range(world + 1)]
+    ks = key[order]
+    lo = [float(ks[bounds[r]]) for r in range(world)]
+    hi = [float(ks[bounds[r + 1] - 1]) for r in range(world)]
+    band = default_halo(pos, k)
+    rank_of = torch.empty(n, dtype=torch.int64, device=dev)
+    for r in range(world):
+        rank_of[order[bounds[r]:bounds[r + 1]]] = r
+    lo_t = torch.tensor(lo, device=dev, dtype=key.dtype)[rank_of]
+    hi_t = torch.tensor(hi, device=dev, dtype=key.dtype)[rank_of]
+    first, last = rank_of == 0, rank_of == world - 1
+    near = ((key > hi_t - band) & ~last) | ((key < lo_t + band) & ~first)
+    idx = torch.nonzero(near).flatten()
+    if idx.numel() == 0:
+        return 0.0
+    g = nat.Grid(pos, k_hint=k)
+    _, d2 = g.knn(pos[idx].contiguous(), k, with_d2=True)
+    dk = d2[:, -1].sqrt()
+    q = key[idx]
+    up = torch.where(last[idx], torch.zeros_like(dk), q + dk - hi_t[idx])
+    down = torch.where(first[idx], torch.zeros_like(dk), lo_t[idx] - q + dk)
+    reach = float(torch.maximum(up, down).max().clamp(min=0))
+    return margin * reach
 
 
 def default_halo(snap_pos: torch.Tensor, k: int, sample: int = 65536, factor: float = 3.0) -> float:

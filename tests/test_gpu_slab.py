@@ -11,6 +11,7 @@ import torch
 
 import pcd_native as nat
 from pcd_slab import LocalTransport, SlabDenoiser, TorchTransport, gather_global, default_halo
+from conftest import report
 
 K, KU, ITERS = 32, 8, 3
 
@@ -433,3 +434,25 @@ def test_mesh_slabs_world2_equal_one_gpu(gpu, tmp_path, fp32):
         assert int(z["halo"]) > 0
         got[z["ids"]] = z["v"]
     np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_cut_halo_covers_the_snapshot_balls_and_is_thinner(gpu):
+    """cut_halo (the default since round 5): every snapshot point's k-ball stays inside its slab widened by the halo,
+    and the halo is far thinner than default_halo's sample-maximum estimate (noise outliers price that one)."""
+    from pcd_slab import SlabPlan, cut_halo
+    pos, _ = _cloud(gpu, 400_000, seed=3)
+    world = 4
+    h = cut_halo(pos, world, K, margin=1.0)
+    hd = default_halo(pos, K)
+    plan = SlabPlan.build(pos, world, h)
+    _, d2 = nat.Grid(pos, k_hint=K).knn(pos, K, with_d2=True)
+    dk = d2[:, -1].sqrt()
+    key = pos[:, plan.axis]
+    lo = torch.tensor(plan.lo, device=gpu)[plan.owner]
+    hi = torch.tensor(plan.hi, device=gpu)[plan.owner]
+    top = plan.owner < world - 1
+    bot = plan.owner > 0
+    assert bool(((key + dk <= hi + h * (1 + 1e-6)) | ~top).all()) and bool(((key - dk >= lo - h * (1 + 1e-6)) | ~bot).all())
+    report(f"cut_halo {h:.4g} vs default_halo {hd:.4g} (x{hd / h:.1f})")
+    assert h < 0.6 * hd
