@@ -310,6 +310,9 @@ static constexpr int kAnchorBS = PCD_ANCHOR_BS;
 #ifndef PCD_ANCHOR_SPLIT
 #define PCD_ANCHOR_SPLIT 1   // 0: one 64-key network; 2: four quarters (A/B at 10M: anchor test 1.29 / 1.26 / 1.31 ms at 0 / 1 / 2)
 #endif
+#ifndef PCD_ANCHOR_PRELOAD
+#define PCD_ANCHOR_PRELOAD 0  // 1: the whole anchor set's blocks loaded with the row's own loads (two-halves variant)
+#endif
 #ifndef PCD_ANCHOR_BATCH
 #define PCD_ANCHOR_BATCH 64   // anchor-set slots gathered per batch (all of them by default)
 #endif
@@ -329,6 +332,17 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
     bool failed = false;
     if (t0 < rm.nq) {
         const int64_t i = rm(t0);
+#if PCD_ANCHOR_PRELOAD
+        // every block of the anchor set issued with the row's own loads (they depend on the row only): the second
+        // half's ranks are not fetched after the first half's keys, one HBM round trip off the critical path
+        v4i pre[KA / 4];
+#pragma unroll
+        for (int g8 = 0; g8 < KA / 8; ++g8) {
+            const v4i* lp = lblock(alist, N, i, g8);
+            pre[2 * g8] = __builtin_nontemporal_load(lp);
+            pre[2 * g8 + 1] = __builtin_nontemporal_load(lp + 1);
+        }
+#endif
         const float4 p4 = pos[i];
         const Vec3 vi = v3(p4.x, p4.y, p4.z);
         const float4 a = anc[i];
@@ -432,8 +446,12 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
                 uint32_t r[32];
 #pragma unroll
                 for (int g8 = 0; g8 < 4; ++g8) {
+#if PCD_ANCHOR_PRELOAD
+                    const v4i x = pre[2 * (4 * h + g8)], y = pre[2 * (4 * h + g8) + 1];
+#else
                     const v4i* lp = lblock(alist, N, i, 4 * h + g8);
                     const v4i x = __builtin_nontemporal_load(lp), y = __builtin_nontemporal_load(lp + 1);
+#endif
                     r[8 * g8 + 0] = (uint32_t)x.x; r[8 * g8 + 1] = (uint32_t)x.y; r[8 * g8 + 2] = (uint32_t)x.z;
                     r[8 * g8 + 3] = (uint32_t)x.w; r[8 * g8 + 4] = (uint32_t)y.x; r[8 * g8 + 5] = (uint32_t)y.y;
                     r[8 * g8 + 6] = (uint32_t)y.z; r[8 * g8 + 7] = (uint32_t)y.w;
