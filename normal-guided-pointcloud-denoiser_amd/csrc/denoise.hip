@@ -310,8 +310,11 @@ static constexpr int kAnchorBS = PCD_ANCHOR_BS;
 #ifndef PCD_ANCHOR_SPLIT
 #define PCD_ANCHOR_SPLIT 1   // 0: one 64-key network; 2: four quarters (A/B at 10M: anchor test 1.29 / 1.26 / 1.31 ms at 0 / 1 / 2)
 #endif
+#ifndef PCD_DENSE_PRE
+#define PCD_DENSE_PRE 1      // the dense radii by a lane-per-row pass before the dense anchoring (k_dense_radius): first iteration 21.1 -> 19.5 ms (A/B at 10M); 2: the query boxes too
+#endif
 #ifndef PCD_ANCHOR_PRELOAD
-#define PCD_ANCHOR_PRELOAD 0  // 1: the whole anchor set's blocks loaded with the row's own loads (two-halves variant)
+#define PCD_ANCHOR_PRELOAD 1  // the whole anchor set's blocks loaded with the row's own loads (two-halves variant): anchor test 1.306 -> 1.29 ms, 211 -> 181 VGPRs
 #endif
 #ifndef PCD_ANCHOR_BATCH
 #define PCD_ANCHOR_BATCH 64   // anchor-set slots gathered per batch (all of them by default)
@@ -1283,7 +1286,16 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     case C:                                                                                                            \
         if (dense) {                                                                                                   \
             if (ev) PCD_HIP(hipEventRecord(ev[1], st));                                                                \
-            if (PCD_DENSE_Q > 0)                                                                                       \
+            if (PCD_DENSE_Q > 0 && PCD_DENSE_PRE) {                                                                    \
+                /* the radii by a lane-per-row pass, into the redo list (idle until the steady iterations) */        \
+                /* (PCD_DENSE_PRE 2: and the query boxes, into f_n -- rewritten by NVT1 after the search) */          \
+                float* rpre = reinterpret_cast<float*>(dn->redo);                                                      \
+                uint4* bpre = PCD_DENSE_PRE >= 2 && !rm.rows ? reinterpret_cast<uint4*>(dn->fn) : nullptr;             \
+                hipLaunchKernelGGL(k_dense_radius, grd, blk, 0, st, gv, P, rm, PCD_RQ_RDENSE, rpre, bpre);             \
+                hipLaunchKernelGGL((k_knn_dense_q<2 * C, (PCD_DENSE_Q > 0 ? PCD_DENSE_Q : 1)>), grd_dq, blk, 0, st, gv, P, N, rm, \
+                                   kstore, PCD_RQ_RDENSE, dn->anc, dn->alist, dn->idx, dn->spill, spill_cnt, nullptr,   \
+                                   nullptr, rpre, bpre);                                                               \
+            } else if (PCD_DENSE_Q > 0)                                                                                \
                 hipLaunchKernelGGL((k_knn_dense_q<2 * C, (PCD_DENSE_Q > 0 ? PCD_DENSE_Q : 1)>), grd_dq, blk, 0, st, gv, P, N, rm, \
                                    kstore, PCD_RQ_RDENSE, dn->anc, dn->alist, dn->idx, dn->spill, spill_cnt);          \
             else                                                                                                       \

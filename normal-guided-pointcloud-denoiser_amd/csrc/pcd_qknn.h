@@ -742,6 +742,30 @@ PCD_DEV void rq_scan_box_q(const GridView& g, const Src& src, const Vec3 (&q)[Q]
 // LIST (steady re-anchoring): the rows of list[0 .. *list_cnt) (the anchor test's failures, in row order, so
 // consecutive entries are spatial neighbours) with the radius of their old anchor, as k_knn_requery<KA, false>; a row
 // without an anchor spills to the wave search.
+// The dense radius of every active row, r_scale h (16 / n)^(1/3) with n the occupancy of the row's cell, one lane a
+// row: the hash probe and the cube root leave the waves of k_knn_dense_q, where every query paid them at full wave
+// width before its box was known (same float arithmetic: the same radius).
+__global__ void k_dense_radius(GridView g, const float4* __restrict__ pos, RowMap rm, float r_scale,
+                               float* __restrict__ out, uint4* __restrict__ box = nullptr) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= rm.nq) return;
+    const float4 p4 = pos[rm(t)];
+    const int cx = min(max(cell_coord(p4.x, g.ox, g.inv_h), 0), g.dx - 1);
+    const int cy = min(max(cell_coord(p4.y, g.oy, g.inv_h), 0), g.dy - 1);
+    const int cz = min(max(cell_coord(p4.z, g.oz, g.inv_h), 0), g.dz - 1);
+    uint32_t s = 0, e = 0;
+    const int n = cell_range(g, cx, cy, cz, s, e) ? (int)(e - s) : 1;
+    const float rs = r_scale * g.h * cbrtf(16.f / (float)n);
+    out[t] = rs;
+    if (box) {   // and the query's cell box (cell_box at rs * 1.0001), 16 bits a coordinate; w = 1: not representable
+        int lo[3], hi[3];
+        cell_box(g, v3(p4.x, p4.y, p4.z), rs * 1.0001f + 1e-30f, lo, hi);
+        const bool fits = hi[0] < 65536 && hi[1] < 65536 && hi[2] < 65536;
+        box[t] = make_uint4((uint32_t)lo[0] | ((uint32_t)lo[1] << 16), (uint32_t)lo[2] | ((uint32_t)hi[0] << 16),
+                            (uint32_t)hi[1] | ((uint32_t)hi[2] << 16), fits ? 0u : 1u);
+    }
+}
+
 template <int KA, int Q, bool LIST = false>
 __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, const float4* __restrict__ pos, int64_t N,
                                                                 RowMap rm, int kstore, float r_scale,
@@ -749,7 +773,9 @@ __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, con
                                                                 int32_t* __restrict__ idx, int32_t* __restrict__ spill,
                                                                 unsigned* __restrict__ spill_cnt,
                                                                 const int32_t* __restrict__ list = nullptr,
-                                                                const unsigned* __restrict__ list_cnt = nullptr) {
+                                                                const unsigned* __restrict__ list_cnt = nullptr,
+                                                                const float* __restrict__ rpre = nullptr,
+                                                                const uint4* __restrict__ bpre = nullptr) {
     constexpr int W = 64;
     __shared__ unsigned long long s_buf[4][Q][RqSurv<W>::n];
     __shared__ RqCells s_cells[4];
@@ -782,6 +808,8 @@ __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, con
                     act[j] = false;
                 }
                 rs[j] = a.w > 0.f ? a.w * PCD_RQ_RSCALE : g.h;
+            } else if (rpre) {
+                rs[j] = rpre[tj];                       // (k_dense_radius)
             } else {
                 const int cx = min(max(cell_coord(q[j].x, g.ox, g.inv_h), 0), g.dx - 1);
                 const int cy = min(max(cell_coord(q[j].y, g.oy, g.inv_h), 0), g.dy - 1);
@@ -792,7 +820,14 @@ __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, con
             }
             cap[j] = ((unsigned long long)__float_as_uint(rs[j] * rs[j]) << 32) | 0xFFFFFFFFull;
             int l3[3], h3[3];
-            cell_box(g, q[j], rs[j] * 1.0001f + 1e-30f, l3, h3);
+            uint4 bx = make_uint4(0u, 0u, 0u, 1u);
+            if (!LIST && bpre) bx = bpre[tj];          // (k_dense_radius)
+            if (bx.w == 0u) {
+                l3[0] = (int)(bx.x & 0xFFFFu); l3[1] = (int)(bx.x >> 16); l3[2] = (int)(bx.y & 0xFFFFu);
+                h3[0] = (int)(bx.y >> 16); h3[1] = (int)(bx.z & 0xFFFFu); h3[2] = (int)(bx.z >> 16);
+            } else {
+                cell_box(g, q[j], rs[j] * 1.0001f + 1e-30f, l3, h3);
+            }
             const int64_t nbox = (int64_t)(h3[0] - l3[0] + 1) * (h3[1] - l3[1] + 1) * (h3[2] - l3[2] + 1);
             clean[j] = nbox <= kRqMaxCells;           // (an oversized box runs alone and spills there)
             any_big = any_big || (act[j] && !clean[j]);
