@@ -311,7 +311,7 @@ static constexpr int kAnchorBS = PCD_ANCHOR_BS;
 #define PCD_ANCHOR_SPLIT 1   // 0: one 64-key network; 2: four quarters (A/B at 10M: anchor test 1.29 / 1.26 / 1.31 ms at 0 / 1 / 2)
 #endif
 #ifndef PCD_DENSE_PRE
-#define PCD_DENSE_PRE 1      // the dense radii by a lane-per-row pass before the dense anchoring (k_dense_radius): first iteration 21.1 -> 19.5 ms (A/B at 10M); 2: the query boxes too
+#define PCD_DENSE_PRE 2      // the dense radii (1) and query boxes (2) by a lane-per-row pass before the dense anchoring (k_dense_radius): first iteration 21.1 -> 19.6 -> 19.1 ms (A/B at 10M)
 #endif
 #ifndef PCD_ANCHOR_PRELOAD
 #define PCD_ANCHOR_PRELOAD 1  // the whole anchor set's blocks loaded with the row's own loads (two-halves variant): anchor test 1.306 -> 1.29 ms, 211 -> 181 VGPRs
