@@ -48,6 +48,23 @@ __global__ void k_xunpack(XField f, const int32_t* __restrict__ rows, int64_t n,
     f.da[r] = v;
     if (f.db) f.db[r] = v;
 }
+// The RCCL path moves 12-byte rows (x, y, z: every exchanged field's w is unused -- positions and unit normals), a
+// quarter less over xGMI than float4 rows; the receiver keeps its own w.
+__global__ void k_xpack3(XField f, const int32_t* __restrict__ rows, int64_t n, float* __restrict__ out) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int32_t r = rows[t];
+    const float4 v = (f.b && ((f.moved >> (f.cls[r] & 31u)) & 1u)) ? f.b[r] : f.a[r];
+    out[3 * t] = v.x; out[3 * t + 1] = v.y; out[3 * t + 2] = v.z;
+}
+__global__ void k_xunpack3(XField f, const int32_t* __restrict__ rows, int64_t n, const float* __restrict__ in) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int32_t r = rows[t];
+    const float x = in[3 * t], y = in[3 * t + 1], z = in[3 * t + 2];
+    f.da[r] = make_float4(x, y, z, f.da[r].w);
+    if (f.db) f.db[r] = make_float4(x, y, z, f.db[r].w);
+}
 
 }  // namespace pcd
 
@@ -88,22 +105,26 @@ static int xchg_begin(pcd_denoiser* dn, pcd_comm* c, hipStream_t st, const XFiel
     const int64_t ns = dn->soff[dn->npeers], nr = dn->roff[dn->npeers];
     PCD_HIP(hipEventRecord(dn->xev_in, st));
     PCD_HIP(hipStreamWaitEvent(xs, dn->xev_in, 0));
-    if (ns > 0) hipLaunchKernelGGL(k_xpack, dim3((unsigned)cdiv(ns, 256)), dim3(256), 0, xs, f, dn->srows, ns, dn->sbuf);
-    PCD_LAUNCH_CHECK();
     dn->xfield = f;
     if (c->nccl) {
+        float* sb = reinterpret_cast<float*>(dn->sbuf);
+        float* rb = reinterpret_cast<float*>(dn->rbuf);
+        if (ns > 0) hipLaunchKernelGGL(k_xpack3, dim3((unsigned)cdiv(ns, 256)), dim3(256), 0, xs, f, dn->srows, ns, sb);
+        PCD_LAUNCH_CHECK();
         PCD_NCCL(ncclGroupStart());
         for (int q = 0; q < dn->npeers; ++q) {
             const int64_t s0 = dn->soff[q], s1 = dn->soff[q + 1], r0 = dn->roff[q], r1 = dn->roff[q + 1];
-            if (s1 > s0) PCD_NCCL(ncclSend(dn->sbuf + s0, (size_t)(s1 - s0) * 4, ncclFloat, dn->peers[q], c->nccl, xs));
-            if (r1 > r0) PCD_NCCL(ncclRecv(dn->rbuf + r0, (size_t)(r1 - r0) * 4, ncclFloat, dn->peers[q], c->nccl, xs));
+            if (s1 > s0) PCD_NCCL(ncclSend(sb + 3 * s0, (size_t)(s1 - s0) * 3, ncclFloat, dn->peers[q], c->nccl, xs));
+            if (r1 > r0) PCD_NCCL(ncclRecv(rb + 3 * r0, (size_t)(r1 - r0) * 3, ncclFloat, dn->peers[q], c->nccl, xs));
         }
         PCD_NCCL(ncclGroupEnd());
-        if (nr > 0) hipLaunchKernelGGL(k_xunpack, dim3((unsigned)cdiv(nr, 256)), dim3(256), 0, xs, f, dn->rrows, nr, dn->rbuf);
+        if (nr > 0) hipLaunchKernelGGL(k_xunpack3, dim3((unsigned)cdiv(nr, 256)), dim3(256), 0, xs, f, dn->rrows, nr, rb);
         PCD_LAUNCH_CHECK();
         PCD_HIP(hipEventRecord(dn->xev_out, xs));
         dn->xpending = true;
     } else {
+        if (ns > 0) hipLaunchKernelGGL(k_xpack, dim3((unsigned)cdiv(ns, 256)), dim3(256), 0, xs, f, dn->srows, ns, dn->sbuf);
+        PCD_LAUNCH_CHECK();
         if (ns > 0) PCD_HIP(hipMemcpyAsync(dn->hs, dn->sbuf, ns * sizeof(float4), hipMemcpyDeviceToHost, xs));
         dn->xbegun = true;
     }
