@@ -358,6 +358,12 @@ def measured_traffic(points, k, ms_per_step):
             "source": tj.get("source", "profiles/traffic.json")}
 
 
+def progress(msg: str):
+    """A progress line on stderr (rank 0 of a multi-rank run): long set-ups stay visibly alive."""
+    if os.environ.get("RANK", "0") == "0":
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def free_port() -> int:
     import socket
     with socket.socket() as sk:
@@ -462,14 +468,17 @@ def main():
         pos = nrm = None
         dt = torch.zeros(1, dtype=torch.float64)
         if rank == 0:
+            progress(f"slab mode: sampling the {total:,}-point cloud on rank 0")
             pos, nrm, diag = make_cloud(total, 3, dev)
             dt[0] = 2 * float(Processor(Pointcloud(pos), k_hint=args.k).meanEdgeLength())
+            progress("d = 2 l computed; planning the slabs")
         dist.broadcast(dt, 0)
         d = float(dt)
         # coverage checked every 10 iterations (a thin halo re-plans and replays, pcd_slab); slabs re-cut by class
         # cost after the second warm-up iteration (rebalance), so the timed region runs on the balanced plan
         tr = TorchTransport(rccl=not args.rehearse_one_gpu)
         sd = SlabDenoiser(pos, nrm, max(args.k, args.k_update), transport=tr, seeding=args.seeding, check_every=10)
+        progress(f"slabs handed out (halo {sd.halo:.4g}); warm-up")
         del pos, nrm
         torch.cuda.empty_cache()
         params = nat.make_params(k=args.k, k_update=args.k_update, d=d)
@@ -498,6 +507,9 @@ def main():
             step()
         if mode == "slab" and args.rebalance and w == min(1, args.warmup - 2):
             sd.rebalance()         # cost-weighted cut from this iteration's classes (next iteration re-anchors)
+            progress("re-cut by class cost")
+        if mode == "slab":
+            progress(f"warm-up iteration {w + 1}/{args.warmup}")
     if mode != "slab":
         fused.set_timing(True)     # per-stage HIP events on the launch stream, every timed iteration
 
@@ -520,6 +532,7 @@ def main():
         return el
 
     if mode == "slab":
+        progress("timed region")
         # the timed iterations carry no coverage check (a host sync + an all-reduce): it runs right after them, and a
         # thin halo there (re-planned and replayed) sends the region round again on the widened plan
         every = sd.check_every
