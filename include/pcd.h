@@ -266,6 +266,12 @@ enum { PCD_STAGE_KNN_NVT1 = 0, PCD_STAGE_NVT2 = 1, PCD_STAGE_PHASE_SUM = 2, PCD_
 int pcd_denoiser_set_rows(pcd_denoiser* dn, const int32_t* rows, int64_t n_rows);
 /* host lo3/hi3: the box the local snapshot covers (null: no check). */
 int pcd_denoiser_set_coverage(pcd_denoiser* dn, const float* lo3, const float* hi3);
+/* Spatial slabs: per-point coverage spheres (DEVICE float [n], caller order; 0 = none; null: clear).  A point whose
+ * k-ball leaves the coverage box is still covered when the ball lies inside the sphere of radius radii[i] around its
+ * position at load -- the slab driver adds every snapshot point of such a sphere to the local snapshot (the sparse
+ * points near a cut, whose balls would otherwise widen every rank's halo).  Replaces nothing in the reference (it is
+ * the exactness condition of Selector.getKNNSelection's KD-tree query over a partitioned snapshot, Selector.py:243). */
+int pcd_denoiser_set_coverage_spheres(pcd_denoiser* dn, const float* radii, void* stream);
 /* one stage; red: device scalars as above (SUM/CENTRE: double[4] Σx,Σy,Σz,count; MAXDIST out / APPLY in:
  * float[1] delta, nullable = local value). */
 int pcd_denoiser_stage(pcd_denoiser* dn, const pcd_denoise_params* p, int stage, int phase, void* red,

@@ -139,6 +139,12 @@ __global__ void k_load(const float* __restrict__ pos, const float* __restrict__ 
     n_s[r] = make_float4(n[3 * i], n[3 * i + 1], n[3 * i + 2], 0.f);
 }
 
+__global__ void k_gather_f32(const float* __restrict__ in, const int32_t* __restrict__ perm, int64_t N,
+                             float* __restrict__ out) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r < N) out[r] = in[perm[r]];
+}
+
 __global__ void k_store(const float4* __restrict__ pos_s, const float4* __restrict__ n_s,
                         const uint8_t* __restrict__ cls_s, const float4* __restrict__ edge_s,
                         const int32_t* __restrict__ perm, int64_t N, float* __restrict__ pos, float* __restrict__ n,
@@ -156,12 +162,26 @@ __global__ void k_store(const float4* __restrict__ pos_s, const float4* __restri
 // the slab widened by the halo).  Disabled when lo > hi on axis 0.
 struct Cover {
     float lo[3], hi[3];
+    // spatial slabs: rows whose snapshot ball the local snapshot holds beyond the box (a sparse point near a cut:
+    // every snapshot point within xr[i] of its load-time position org[i] is local; 0 = none)
+    const float* xr = nullptr;
+    const float4* org = nullptr;
     PCD_DEV bool enabled() const { return !(lo[0] > hi[0]); }
     PCD_DEV bool holds(Vec3 q, float d2) const {
         if (lo[0] > hi[0]) return true;
         const float r = sqrtf(d2) * 1.000001f + 1e-30f;
         return q.x - r >= lo[0] && q.x + r <= hi[0] && q.y - r >= lo[1] && q.y + r <= hi[1] && q.z - r >= lo[2] &&
                q.z + r <= hi[2];
+    }
+    // row i's k-ball (centre q, squared radius d2) lies inside the box, or inside the row's own sphere
+    PCD_DEV bool holds_row(int64_t i, Vec3 q, float d2) const {
+        if (holds(q, d2)) return true;
+        if (!xr) return false;
+        const float R = xr[i];
+        if (!(R > 0.f)) return false;
+        const float4 o = org[i];
+        const float m = sqrtf(sq3(q - v3(o.x, o.y, o.z))) * 1.000001f + sqrtf(d2) * 1.000001f + 1e-30f;
+        return m <= R * (1.f - 1e-6f);
     }
 };
 
@@ -196,7 +216,7 @@ PCD_DEV void k1_epilogue(const float4* __restrict__ pos, const float4* __restric
     }
     store_list<K, true>(idx, N, i, kstore, l);   // streamed: keep L2 for the gathers
     if (bad) atomicOr(err, 1);
-    if (!cov.holds(vi, dk)) atomicOr(err, 2);
+    if (!cov.holds_row(i, vi, dk)) atomicOr(err, 2);
     band.mark(t0, vi, dk);
 #ifdef PCD_EXP_NONVT
     const float4 n4 = nrm[i];
@@ -620,7 +640,7 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
 #pragma unroll
         for (int t = 0; t < K; ++t)
             if (t == kstore - 1) dk = dist2(vi, g.pts[l[t]]);
-        if (!cov.holds(vi, dk)) atomicOr(err, 2);
+        if (!cov.holds_row(i, vi, dk)) atomicOr(err, 2);
         band.mark(t0, vi, dk);
     }
     // 4 neighbours in flight per batch (8 measured 0.06 ms slower at 10M: the VGPRs of 8 rows in flight)
@@ -1094,6 +1114,7 @@ struct pcd_denoiser {
     int kcap = 0;                 // columns of the stored kNN list
     float4 *pos[2] = {nullptr, nullptr}, *nrm = nullptr, *fn = nullptr, *edge = nullptr;
     float4* orig = nullptr;       // positions at load(): the global clamp's reference (pcd_denoise_params)
+    float* xrad = nullptr;        // spatial slabs: per-row coverage sphere radius (Cover::xr), null: none
     int cur = 0;                  // pos[cur] holds the current positions
     int32_t* idx = nullptr;
     uint8_t* cls = nullptr;
@@ -1549,6 +1570,7 @@ int pcd_denoiser_destroy(pcd_denoiser* dn) {
     destroy_slab_state(dn);
     destroy_cpsd_state(dn);
     (void)hipFree(dn->pos[0]); (void)hipFree(dn->pos[1]); (void)hipFree(dn->nrm); (void)hipFree(dn->fn);
+    (void)hipFree(dn->xrad);
     (void)hipFree(dn->edge); (void)hipFree(dn->orig); (void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part);
     (void)hipFree(dn->red); (void)hipFree(dn->gscal); (void)hipFree(dn->err);
     (void)hipFree(dn->anc); (void)hipFree(dn->alist); (void)hipFree(dn->redo); (void)hipFree(dn->spill);
@@ -1590,6 +1612,8 @@ int pcd_denoiser_set_coverage(pcd_denoiser* dn, const float* lo3, const float* h
     PCD_CHECK_ARG(dn != nullptr, "null denoiser");
     if (!lo3 || !hi3) {
         dn->cov = Cover{{1.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+        dn->cov.xr = dn->xrad;
+        dn->cov.org = dn->orig;
         return PCD_OK;
     }
     for (int a = 0; a < 3; ++a) {
@@ -1597,6 +1621,29 @@ int pcd_denoiser_set_coverage(pcd_denoiser* dn, const float* lo3, const float* h
         dn->cov.lo[a] = lo3[a];
         dn->cov.hi[a] = hi3[a];
     }
+    dn->cov.xr = dn->xrad;
+    dn->cov.org = dn->orig;
+    return PCD_OK;
+}
+
+int pcd_denoiser_set_coverage_spheres(pcd_denoiser* dn, const float* radii, void* stream) {
+    PCD_CHECK_ARG(dn != nullptr, "null denoiser");
+    hipStream_t st = as_stream(stream);
+    if (!radii) {
+        PCD_HIP(hipStreamSynchronize(st));
+        (void)hipFree(dn->xrad);
+        dn->xrad = nullptr;
+        dn->cov.xr = nullptr;
+        return PCD_OK;
+    }
+    if (!dn->xrad && hipMalloc(&dn->xrad, dn->n * sizeof(float)) != hipSuccess)
+        return fail(PCD_ERR_OOM, "pcd_denoiser_set_coverage_spheres");
+    // caller order -> the denoiser's sorted rows (the load permutation)
+    hipLaunchKernelGGL(k_gather_f32, dim3((unsigned)cdiv(dn->n, 256)), dim3(256), 0, st, radii, dn->g->perm, dn->n,
+                       dn->xrad);
+    PCD_LAUNCH_CHECK();
+    dn->cov.xr = dn->xrad;
+    dn->cov.org = dn->orig;
     return PCD_OK;
 }
 

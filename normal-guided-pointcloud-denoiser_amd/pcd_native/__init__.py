@@ -102,6 +102,7 @@ _SIGS = {
     "pcd_denoiser_probe_store": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_denoiser_set_rows": (c_int, [c_void_p, c_void_p, c_int64]),
     "pcd_denoiser_set_coverage": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "pcd_denoiser_set_coverage_spheres": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pcd_denoiser_stage": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "pcd_denoiser_pack": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "pcd_denoiser_unpack": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
@@ -402,6 +403,16 @@ class FusedDenoiser:
         lo3 = (c_float * 3)(*[float(v) for v in lo])
         hi3 = (c_float * 3)(*[float(v) for v in hi])
         check(lib().pcd_denoiser_set_coverage(self.handle, lo3, hi3), "pcd_denoiser_set_coverage")
+
+    def set_coverage_spheres(self, radii=None):
+        """Per-point coverage spheres (float32 [n], caller order, 0 = none; None clears): pcd_denoiser_set_coverage_spheres."""
+        r = None if radii is None else f32(radii)
+        if r is not None:
+            assert r.dim() == 1 and r.numel() == self.grid.n
+        check(lib().pcd_denoiser_set_coverage_spheres(self.handle, ptr(r), c_void_p(stream_ptr())),
+              "pcd_denoiser_set_coverage_spheres")
+        if r is not None:
+            torch.cuda.current_stream().synchronize()
 
     def stage(self, params: DenoiseParams, stage: int, phase: int = 0, red: torch.Tensor = None):
         check(lib().pcd_denoiser_stage(self.handle, ctypes.byref(params), int(stage), int(phase), ptr(red),

@@ -42,6 +42,31 @@ import pcd_native as nat
 
 # ----------------------------------------------------------------------------------------------- partition
 @dataclass
+class Spheres:
+    """Coverage spheres of the sparse points near a cut (cut_spheres): centre ids (global), radii, and the snapshot
+    members of each sphere (CSR over the centres, global ids) -- local to the centre's owner."""
+    ids: torch.Tensor
+    radii: torch.Tensor
+    slices: torch.Tensor
+    members: torch.Tensor
+
+    @staticmethod
+    def around(snap: torch.Tensor, ids: torch.Tensor, radii: torch.Tensor, k_hint: int = 16) -> "Spheres":
+        dev = nat.device()
+        if ids.numel() == 0:
+            z = torch.zeros(0, dtype=torch.int64, device=snap.device)
+            return Spheres(z, torch.zeros(0, device=snap.device), torch.zeros(1, dtype=torch.int64, device=snap.device), z)
+        g = nat.Grid(snap.to(dev), k_hint=k_hint)
+        # (membership at a hair over the radius: the coverage test asks for the ball strictly inside it)
+        sl, j = g.radius(snap.to(dev)[ids.to(dev)].contiguous(), (radii.to(dev) * 1.0001).contiguous())
+        return Spheres(ids.to(snap.device), radii.to(snap.device, torch.float32), sl.to(snap.device),
+                       j.to(snap.device))
+
+    def scaled(self, snap: torch.Tensor, factor: float) -> "Spheres":
+        return Spheres.around(snap, self.ids, self.radii * factor)
+
+
+@dataclass
 class SlabPlan:
     """Owned / halo membership of every rank, identical on all ranks (computed from the same snapshot)."""
     world: int
@@ -51,12 +76,14 @@ class SlabPlan:
     lo: list                                    # per rank: min coordinate of the owned points on `axis`
     hi: list                                    # per rank: max coordinate
     local: list = field(default_factory=list)   # per rank: int64 global indices of owned + halo, ascending
+    spheres: "Spheres | None" = None            # points whose k-ball reaches past the band halo (cut_spheres)
 
     @staticmethod
     def build(snap: torch.Tensor, world: int, halo: float, axis: int | None = None,
-              weights: torch.Tensor | None = None) -> "SlabPlan":
+              weights: torch.Tensor | None = None, spheres: "Spheres | None" = None) -> "SlabPlan":
         """weights (optional, [N] >= 0, identical on every rank): cut at quantiles of the cumulative weight along the
-        axis instead of equal point counts (each rank still owns at least one point)."""
+        axis instead of equal point counts (each rank still owns at least one point).  spheres (optional): every
+        member of a sphere is local to the owner of its centre, beyond the band."""
         snap = snap.detach()
         n = snap.size(0)
         assert world >= 1 and n >= world, "need at least one point per rank"
@@ -85,8 +112,14 @@ class SlabPlan:
             hi.append(float(ks[-1]))
         for r in range(world):
             inside = (key >= lo[r] - halo) & (key <= hi[r] + halo)
+            if spheres is not None and spheres.ids.numel():
+                mine = owner[spheres.ids] == r
+                if bool(mine.any()):
+                    seg = torch.repeat_interleave(mine, spheres.slices.diff())
+                    inside = inside.clone()
+                    inside[spheres.members[seg]] = True
             local.append(torch.nonzero(inside | (owner == r)).flatten())
-        return SlabPlan(world, axis, float(halo), owner, lo, hi, local)
+        return SlabPlan(world, axis, float(halo), owner, lo, hi, local, spheres)
 
     def coverage(self, r: int):
         """Box the rank's local snapshot covers: the slab widened by the halo on `axis` (open ends at the outer
@@ -231,7 +264,7 @@ class LocalTransport:
 class HipSlabEngine:
     """libpcd's fused loop over one rank's local snapshot (owned + halo), driven stage by stage."""
 
-    def __init__(self, local_pos, local_n, owned_local, k_max, origin, cell, coverage, seeding=True):
+    def __init__(self, local_pos, local_n, owned_local, k_max, origin, cell, coverage, seeding=True, spheres=None):
         dev = nat.device()
         self.device = dev
         self.grid = nat.Grid(local_pos.to(dev), cell=cell, origin=origin)
@@ -246,6 +279,8 @@ class HipSlabEngine:
         # every local point owned (one rank): all rows, no row list (the single-GPU launch shapes)
         self.fused.set_rows(None if own_rows.numel() == self.n else own_rows)
         self.fused.set_coverage(*coverage)
+        if spheres is not None:
+            self.fused.set_coverage_spheres(spheres.to(dev))      # (local order: the loaded rows' order)
         self.red4 = torch.zeros(4, dtype=torch.float64, device=dev)
         self.red1 = torch.zeros(1, dtype=torch.float32, device=dev)
 
@@ -326,6 +361,7 @@ class RankShare:
     halo: float
     axis: int
     state: tuple | None = None          # (pos, n) [nl, 3] of the current iterate to take over (a re-plan)
+    xr: torch.Tensor | None = None      # float32 [nl]: coverage sphere radius of each local point (0: none)
 
 
 def _share(plan: SlabPlan, r: int, snap_pos, snap_n, lattice, state=None) -> RankShare:
@@ -362,8 +398,18 @@ def _share(plan: SlabPlan, r: int, snap_pos, snap_n, lattice, state=None) -> Ran
             hi[plan.axis] = float(np.nextafter(np.float32(plan.hi[r]), np.float32(-np.inf)))
         own_box = (lo, hi)
     st = None if state is None else (state[0][local.to(state[0].device)], state[1][local.to(state[1].device)])
+    xr = None
+    sp = plan.spheres
+    if sp is not None and sp.ids.numel():
+        mine = plan.owner[sp.ids] == r
+        if bool(mine.any()):
+            if to_local is None:
+                to_local = torch.full((plan.owner.numel(),), -1, dtype=torch.int64, device=local.device)
+                to_local[local] = torch.arange(local.numel(), device=local.device)
+            xr = torch.zeros(local.numel(), dtype=torch.float32, device=local.device)
+            xr[to_local[sp.ids[mine]]] = sp.radii[mine].to(local.device)
     return RankShare(local, owned_local, snap_pos[local], snap_n[local], peers, send_local, recv_local,
-                     plan.coverage(r), own_box, lattice, plan.halo, plan.axis, st)
+                     plan.coverage(r), own_box, lattice, plan.halo, plan.axis, st, xr)
 
 
 class SlabDenoiser:
@@ -380,9 +426,11 @@ class SlabDenoiser:
     halo_growth / max_replans: the thin-halo recovery."""
 
     def __init__(self, snap_pos, snap_n, k_max, transport=None, halo=None, engine_factory=None, seeding=True,
-                 k_hint=None, check_every=1, halo_growth=2.0, max_replans=4, weights=None, native=None):
+                 k_hint=None, check_every=1, halo_growth=2.0, max_replans=4, weights=None, native=None,
+                 sphere_quantile=0.999):
         """native: one pcd_slab_iterate call per iteration over libpcd's own transport (default for the HIP engine);
-        False: the same stages driven from Python over torch.distributed."""
+        False: the same stages driven from Python over torch.distributed.  sphere_quantile: the default halo covers
+        this quantile of the near-face k-ball reaches; the points beyond it keep coverage spheres (cut_spheres)."""
         self.t = transport or LocalTransport()
         rank, world = self.t.rank, self.t.world
         # cell lattice of the ranks' snapshot indices: the fused loop's (pcd_native.fused_k_hint) unless given
@@ -396,11 +444,16 @@ class SlabDenoiser:
         if rank == 0:
             self.snap_pos, self.snap_n = snap_pos.detach().contiguous(), snap_n.detach().contiguous()
             self.dev = self.snap_pos.device
+            self._spheres = None
             if halo is None:
-                halo = cut_halo(self.snap_pos, world, k_max) if world > 1 else 0.0
+                if world > 1:
+                    halo, sid, srad = cut_spheres(self.snap_pos, world, k_max, quantile=sphere_quantile)
+                    self._spheres = Spheres.around(self.snap_pos, sid, srad) if engine_factory is None else None
+                else:
+                    halo = 0.0
             self._lattice = (nat.grid_params(self.snap_pos.to(nat.device()), k_hint=self.k_hint)
                              if engine_factory is None else ([0.0, 0.0, 0.0], 0.0))
-            plan = SlabPlan.build(self.snap_pos, world, halo, weights=weights)
+            plan = SlabPlan.build(self.snap_pos, world, halo, weights=weights, spheres=self._spheres)
             nt = torch.tensor([self.snap_pos.size(0)], dtype=torch.int64)
         else:
             self.snap_pos = self.snap_n = None
@@ -435,19 +488,20 @@ class SlabDenoiser:
         own = s.own_box or ([nan] * 3, [nan] * 3)
         flt = torch.tensor(list(s.coverage[0]) + list(s.coverage[1]) + list(own[0]) + list(own[1])
                            + list(s.lattice[0]) + [s.lattice[1], s.halo, float(s.axis)], dtype=torch.float64)
-        cols = [s.pos, s.n] + (list(s.state) if s.state is not None else [])
+        cols = [s.pos, s.n] + (list(s.state) if s.state is not None else []) + \
+               ([s.xr[:, None]] if s.xr is not None else [])
         rows = torch.cat([c.to(self.dev, torch.float32) for c in cols], 1)
         head = torch.tensor([s.local.numel(), s.owned_local.numel(), len(s.peers), int(s.state is not None),
-                             ints.numel(), 0, 0, 0], dtype=torch.int64)
+                             ints.numel(), int(s.xr is not None), 0, 0], dtype=torch.int64)
         for t in (head, ints, flt, rows):
             self._p2p_send(t, dst)
 
     def _recv_share(self) -> RankShare:
         head = self._p2p_recv((8,), torch.int64, 0).cpu().tolist()
-        nl, no, npeers, has_state, nints = head[:5]
+        nl, no, npeers, has_state, nints, has_xr = head[:6]
         ints = self._p2p_recv((nints,), torch.int64, 0).to(self.dev)
         flt = self._p2p_recv((20,), torch.float64, 0).cpu().tolist()
-        rows = self._p2p_recv((nl, 12 if has_state else 6), torch.float32, 0).to(self.dev)
+        rows = self._p2p_recv((nl, (12 if has_state else 6) + (1 if has_xr else 0)), torch.float32, 0).to(self.dev)
         o = 0
         local, o = ints[o:o + nl], o + nl
         owned_local, o = ints[o:o + no], o + no
@@ -463,8 +517,9 @@ class SlabDenoiser:
             o += c
         own = None if flt[6] != flt[6] else (flt[6:9], flt[9:12])
         st = (rows[:, 6:9], rows[:, 9:12]) if has_state else None
+        xr = rows[:, -1].contiguous() if has_xr else None
         return RankShare(local, owned_local, rows[:, 0:3], rows[:, 3:6], peers, send_local, recv_local,
-                         (flt[0:3], flt[3:6]), own, (flt[12:15], flt[15]), flt[16], int(flt[17]), st)
+                         (flt[0:3], flt[3:6]), own, (flt[12:15], flt[15]), flt[16], int(flt[17]), st, xr)
 
     def _gather_to0(self, x: torch.Tensor):
         """Per-point values of every rank's own points (owned-local order, [n_own, c] float32) -> the global
@@ -501,7 +556,7 @@ class SlabDenoiser:
         self.owned_global = self.local[self.owned_local]
         if self.engine_factory is None:
             self.e = HipSlabEngine(s.pos, s.n, self.owned_local, self.k_max, s.lattice[0], s.lattice[1], s.coverage,
-                                   self.seeding)
+                                   self.seeding, spheres=s.xr)
         else:
             self.e = self.engine_factory(s.pos, s.n, self.owned_local, self.k_max, s.coverage)
         if s.state is not None:
@@ -542,8 +597,11 @@ class SlabDenoiser:
             state = self._global_state(*self._owned_state_now())
         plan = None
         if self.t.rank == 0:
+            if halo is not None and self._spheres is not None and self.plan.halo > 0:
+                self._spheres = self._spheres.scaled(self.snap_pos, halo / self.plan.halo)   # (widened alike)
             halo = self.plan.halo if halo is None else halo
-            plan = SlabPlan.build(self.snap_pos, self.t.world, halo, axis=self.plan.axis, weights=weights)
+            plan = SlabPlan.build(self.snap_pos, self.t.world, halo, axis=self.plan.axis, weights=weights,
+                                  spheres=self._spheres)
         self._setup(plan, state)
 
     def _any_rank(self, flag: bool) -> bool:
@@ -686,19 +744,29 @@ class SlabDenoiser:
         return self.owned_global, pos[idx], n[idx]
 
 
-def cut_halo(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, axis: int | None = None) -> float:
-    """The halo the equal-count cut into `world` slabs needs at the snapshot, times `margin` for the drift of later
-    iterations: every snapshot point's k-ball (radius d_k, its k-th neighbour distance) must lie inside its slab
-    widened by the halo on the cut axis, so the halo is the largest reach of a ball past its slab's faces,
-    max_q (q + d_k(q) - hi_r, lo_r - q + d_k(q)) over the points near a face.  The balls that reach farthest belong
-    to the sparsest points near a cut (noise outliers), which default_halo's sample maximum prices everywhere three
-    times over.  Only the points within default_halo of a face are searched.  The coverage check still reports any
-    later ball that leaves the halo (a re-plan widens it)."""
+def cut_spheres(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, quantile: float = 0.999,
+                axis: int | None = None):
+    """(band halo, sphere centre ids, sphere radii) for the equal-count cut: the band is `margin` x the `quantile` of
+    the near-face reaches (cut_halo's per-point requirement); every point whose ball reaches farther keeps a
+    sphere of radius margin x d_k around itself instead (all of its snapshot members local to its owner), so a few
+    sparse points near a cut no longer set every rank's halo (at 80M points on 8 ranks the max-reach halo held ~half
+    as many halo rows as owned ones)."""
+    idx, reach, dk = _cut_reach(snap_pos, world, k, axis)
+    if idx.numel() == 0:
+        z = torch.zeros(0, dtype=torch.int64)
+        return 0.0, z, torch.zeros(0)
+    r = reach.clamp(min=0)
+    rs = torch.sort(r).values                        # (torch.quantile refuses inputs past 16M elements)
+    band = margin * max(float(rs[int(quantile * (rs.numel() - 1))]), float(torch.sort(dk).values[dk.numel() // 2]))
+    out = margin * r > band
+    return band, idx[out], margin * dk[out]
+
+
+def _cut_reach(snap_pos: torch.Tensor, world: int, k: int, axis: int | None = None):
+    """Per point near a face of the equal-count cut: (global id, reach of its k-ball past its slab's faces, d_k)."""
     dev = nat.device()
     pos = snap_pos.to(dev)
     n = pos.size(0)
-    if world == 1:
-        return 0.0
     if axis is None:
         axis = int(torch.argmax(pos.max(0).values - pos.min(0).values))
     key = pos[:, axis].contiguous()
@@ -717,15 +785,30 @@ def cut_halo(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, a
     near = ((key > hi_t - band) & ~last) | ((key < lo_t + band) & ~first)
     idx = torch.nonzero(near).flatten()
     if idx.numel() == 0:
-        return 0.0
+        return idx, torch.zeros(0, device=dev), torch.zeros(0, device=dev)
     g = nat.Grid(pos, k_hint=k)
     _, d2 = g.knn(pos[idx].contiguous(), k, with_d2=True)
     dk = d2[:, -1].sqrt()
     q = key[idx]
     up = torch.where(last[idx], torch.zeros_like(dk), q + dk - hi_t[idx])
     down = torch.where(first[idx], torch.zeros_like(dk), lo_t[idx] - q + dk)
-    reach = float(torch.maximum(up, down).max().clamp(min=0))
-    return margin * reach
+    return idx, torch.maximum(up, down), dk
+
+
+def cut_halo(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, axis: int | None = None) -> float:
+    """The halo the equal-count cut into `world` slabs needs at the snapshot, times `margin` for the drift of later
+    iterations: every snapshot point's k-ball (radius d_k, its k-th neighbour distance) must lie inside its slab
+    widened by the halo on the cut axis, so the halo is the largest reach of a ball past its slab's faces,
+    max_q (q + d_k(q) - hi_r, lo_r - q + d_k(q)) over the points near a face.  The balls that reach farthest belong
+    to the sparsest points near a cut (noise outliers), which default_halo's sample maximum prices everywhere three
+    times over.  Only the points within default_halo of a face are searched.  The coverage check still reports any
+    later ball that leaves the halo (a re-plan widens it)."""
+    if world == 1:
+        return 0.0
+    idx, reach, _ = _cut_reach(snap_pos, world, k, axis)
+    if idx.numel() == 0:
+        return 0.0
+    return margin * float(reach.max().clamp(min=0))
 
 
 def default_halo(snap_pos: torch.Tensor, k: int, sample: int = 65536, factor: float = 3.0) -> float:

@@ -65,7 +65,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=False, native=None):
+def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=False, native=None, sq=0.999):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -80,7 +80,7 @@ def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=F
             c = np.load(cloud_path)
             pos, nrm = torch.from_numpy(c["pos"]).to(dev), torch.from_numpy(c["n"]).to(dev)
         tr = TorchTransport(rccl=backend == "rccl")
-        sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K, native=native)
+        sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K, native=native, sphere_quantile=sq)
         if native is not False:
             assert sd.comm.info() == {"world": world, "rank": rank,
                                       "transport": "rccl" if backend == "rccl" else "host"}
@@ -88,7 +88,8 @@ def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=F
         sd.check()
         p, n = gather_global(sd.owned_state(), sd.n_total, tr)
         if rank == 0:
-            np.savez(out_path, pos=p.numpy(), n=n.numpy(), halo=sd.halo_points)
+            np.savez(out_path, pos=p.numpy(), n=n.numpy(), halo=sd.halo_points, replans=sd.replans,
+                     spheres=0 if sd.plan.spheres is None else int(sd.plan.spheres.ids.numel()))
     finally:
         dist.destroy_process_group()
 
@@ -456,3 +457,24 @@ def test_cut_halo_covers_the_snapshot_balls_and_is_thinner(gpu):
     assert bool(((key + dk <= hi + h * (1 + 1e-6)) | ~top).all()) and bool(((key - dk >= lo - h * (1 + 1e-6)) | ~bot).all())
     report(f"cut_halo {h:.4g} vs default_halo {hd:.4g} (x{hd / h:.1f})")
     assert h < 0.6 * hd
+
+
+@pytest.mark.gpu
+def test_hip_slab_world4_coverage_spheres_match_one_gpu(gpu, tmp_path):
+    """The band halo at the MEDIAN near-face reach (sphere_quantile=0.5): half the points near a cut keep their own
+    coverage sphere (every snapshot point of it local to their owner, pcd_denoiser_set_coverage_spheres), four ranks
+    sharing the GPU -- no re-plan, and the one-GPU result within 1e-6 x bbox."""
+    import torch.multiprocessing as mp
+    pos, nrm = _cloud(gpu)
+    d = _d(pos)
+    out, cloud = str(tmp_path / "sph4.npz"), str(tmp_path / "cloud.npz")
+    np.savez(cloud, pos=pos.cpu().numpy(), n=nrm.cpu().numpy())
+    mp.spawn(_worker, args=(4, _free_port(), out, cloud, d, "gloo", False, None, 0.5), nprocs=4, join=True)
+    res = np.load(out)
+    report(f"coverage spheres: {int(res['spheres'])} spheres, halo rows on rank 0 {int(res['halo'])}, "
+           f"replans {int(res['replans'])}")
+    assert int(res["spheres"]) > 100 and int(res["replans"]) == 0
+    rp, rn = _fused(pos, nrm, d)
+    bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
+    np.testing.assert_allclose(res["pos"], rp, rtol=0, atol=1e-6 * bbox)
+    np.testing.assert_allclose(res["n"], rn, rtol=0, atol=1e-5)
