@@ -453,6 +453,7 @@ class SlabDenoiser:
                     halo = 0.0
             self._lattice = (nat.grid_params(self.snap_pos.to(nat.device()), k_hint=self.k_hint)
                              if engine_factory is None else ([0.0, 0.0, 0.0], 0.0))
+            self._weights = weights                 # (the cut's cost weights: a halo re-plan keeps them)
             plan = SlabPlan.build(self.snap_pos, world, halo, weights=weights, spheres=self._spheres)
             nt = torch.tensor([self.snap_pos.size(0)], dtype=torch.int64)
         else:
@@ -600,7 +601,9 @@ class SlabDenoiser:
             if halo is not None and self._spheres is not None and self.plan.halo > 0:
                 self._spheres = self._spheres.scaled(self.snap_pos, halo / self.plan.halo)   # (widened alike)
             halo = self.plan.halo if halo is None else halo
-            plan = SlabPlan.build(self.snap_pos, self.t.world, halo, axis=self.plan.axis, weights=weights,
+            if weights is not None:
+                self._weights = weights
+            plan = SlabPlan.build(self.snap_pos, self.t.world, halo, axis=self.plan.axis, weights=self._weights,
                                   spheres=self._spheres)
         self._setup(plan, state)
 
@@ -745,10 +748,10 @@ class SlabDenoiser:
 
 
 def cut_spheres(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, quantile: float = 0.999,
-                axis: int | None = None):
+                axis: int | None = None, sphere_margin: float = 1.5):
     """(band halo, sphere centre ids, sphere radii) for the equal-count cut: the band is `margin` x the `quantile` of
     the near-face reaches (cut_halo's per-point requirement); every point whose ball reaches farther keeps a
-    sphere of radius margin x d_k around itself instead (all of its snapshot members local to its owner), so a few
+    sphere of radius sphere_margin x d_k around itself instead (all of its snapshot members local to its owner), so a few
     sparse points near a cut no longer set every rank's halo (at 80M points on 8 ranks the max-reach halo held ~half
     as many halo rows as owned ones)."""
     idx, reach, dk = _cut_reach(snap_pos, world, k, axis)
@@ -759,7 +762,7 @@ def cut_spheres(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25
     rs = torch.sort(r).values                        # (torch.quantile refuses inputs past 16M elements)
     band = margin * max(float(rs[int(quantile * (rs.numel() - 1))]), float(torch.sort(dk).values[dk.numel() // 2]))
     out = margin * r > band
-    return band, idx[out], margin * dk[out]
+    return band, idx[out], sphere_margin * dk[out]
 
 
 def _cut_reach(snap_pos: torch.Tensor, world: int, k: int, axis: int | None = None):
