@@ -34,7 +34,7 @@ def main():
         ts.append(e0.elapsed_time(e1))
         st = fd.tile_stats()
         del fd
-    print(f"dense K1 stage at {n:,} points: {' '.join(f'{t:.2f}' for t in ts)} ms  (spilled {st['spilled']})", flush=True)
+    print(f"dense K1 stage at {n:,} points: {' '.join(f'{t:.2f}' for t in ts)} ms  (spilled {st['spilled']}, big box {st['spilled_big_box']}, ambiguous {st['spilled_ambiguous']})", flush=True)
 
 
 if __name__ == "__main__":
