@@ -93,6 +93,19 @@ static constexpr float kEps = 5.9604644775390625e-08f;      // slamch('E') = 2^-
 static constexpr float kSafmin = 1.17549435e-38f;          // slamch('S')
 static constexpr float kSafmn2 = 4.4408920985006262e-16f;  // 2^-51 (slartg scaling bounds)
 static constexpr float kSafmx2 = 2.2517998136852480e+15f;
+// ssteqr's block scaling bounds: ssfmax = sqrt(1 / safmin) / 3, ssfmin = sqrt(safmin) / eps² = 2^-15.  A block whose
+// largest |d|, |e| lies outside them is scaled to the bound (slascl: one multiplication by bound / anorm) before its
+// QL/QR iteration and scaled back after it -- covariance-like tensors (PCA normals, the CPSD position voting) of
+// small point spacings land below ssfmin
+static constexpr float kSsfmax = 3.07445734e+18f;
+static constexpr float kSsfmin = 3.0517578125e-05f;
+// the scale factor of a block (1 when none applies) and its inverse, both as slascl forms them (cto / cfrom)
+PCD_DEV float block_scale(float anorm) {
+    return anorm > kSsfmax ? ldiv(kSsfmax, anorm) : (anorm < kSsfmin ? ldiv(kSsfmin, anorm) : 1.f);
+}
+PCD_DEV float block_unscale(float anorm) {
+    return anorm > kSsfmax ? ldiv(anorm, kSsfmax) : (anorm < kSsfmin ? ldiv(anorm, kSsfmin) : 1.f);
+}
 
 PCD_DEV float fsign(float a, float b) { return b >= 0.f ? fabsf(a) : -fabsf(a); }
 PCD_DEV float slapy2(float x, float y) {
@@ -154,13 +167,15 @@ PCD_DEV void slaev2(float a, float b, float c, float& rt1, float& rt2, float& cs
     if (sgn1 == sgn2) { const float tn = cs1; cs1 = -sn1; sn1 = tn; }
 }
 // slasr('R', 'V', dir): rotation j acts on columns (j, j+1) of Z, for j in [j0, j0+cnt-1)
+// MKL's slasr fuses each update into one fma around the second product (measured against mkl_lapack_ssteqr, 100 % bitwise):
+//   z_{j+1} = fma(c, t, -(s z_j)),  z_j = fma(s, t, c z_j)
 PCD_DEV void rot_cols(float Z[3][3], int j, float ct, float st) {
     if (ct == 1.f && st == 0.f) return;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        const float t = Z[i][j + 1];
-        Z[i][j + 1] = ct * t - st * Z[i][j];
-        Z[i][j] = st * t + ct * Z[i][j];
+        const float t = Z[i][j + 1], z = Z[i][j];
+        Z[i][j + 1] = fmaf(ct, t, -(st * z));
+        Z[i][j] = fmaf(st, t, ct * z);
     }
 }
 
@@ -174,7 +189,7 @@ PCD_DEV void rot_cols_c(float Z[3][3], int j, float ct, float st) {   // rot_col
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const float t = Z[i][j + 1], z = Z[i][j];
-        const float n1 = ct * t - st * z, n0 = st * t + ct * z;
+        const float n1 = fmaf(ct, t, -(st * z)), n0 = fmaf(st, t, ct * z);   // rot_cols' fma pattern
         Z[i][j + 1] = id ? t : n1;
         Z[i][j] = id ? z : n0;
     }
@@ -199,12 +214,27 @@ PCD_DEV void tail2r(bool J1, float d[3], float e[2], float Z[3][3]) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const float t = J1 ? Z[i][2] : Z[i][1], z = J1 ? Z[i][1] : Z[i][0];
-        const float n1 = id ? t : c * t - s * z, n0 = id ? z : s * t + c * z;
+        const float n1 = id ? t : fmaf(c, t, -(s * z)), n0 = id ? z : fmaf(s, t, c * z);
         if (J1) { Z[i][2] = n1; Z[i][1] = n0; } else { Z[i][1] = n1; Z[i][0] = n0; }
     }
     if (J1) { d[1] = rt1; d[2] = rt2; e[1] = 0.f; } else { d[0] = rt1; d[1] = rt2; e[0] = 0.f; }
 }
-PCD_DEV void ql_sweep3(float d[3], float e[2], float Z[3][3]) {   // l = 0, m = 2
+// rot_cols_c in a lane's own frame: in the mirrored (QR) frame the pair (j, j+1) holds the original columns
+// (j'+1, j') and the original rotation's sine is -st, so the fused product falls on the other column -- the same
+// two fmas as the original-frame rotation, operands exchanged (bit-identical to LAPACK's QR sweep under MKL's fmas)
+PCD_DEV void rot_cols_m(float Z[3][3], int j, float ct, float st, bool mir) {
+    const bool id = (ct == 1.f && st == 0.f);
+    const float ss = mir ? -st : st;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float a = Z[i][j], b = Z[i][j + 1];
+        const float x = mir ? a : b, y = mir ? b : a;
+        const float first = fmaf(ct, x, -(ss * y)), second = fmaf(ss, x, ct * y);
+        Z[i][j + 1] = id ? b : (mir ? second : first);
+        Z[i][j] = id ? a : (mir ? first : second);
+    }
+}
+PCD_DEV void ql_sweep3(float d[3], float e[2], float Z[3][3], bool mir) {   // l = 0, m = 2 (mir: the QR frame)
     float p = d[0];
     float g = ldiv(d[1] - p, 2.f * e[0]);
     float r = slapy2(g, 1.f);
@@ -227,48 +257,23 @@ PCD_DEV void ql_sweep3(float d[3], float e[2], float Z[3][3]) {   // l = 0, m = 
     p = s * r;
     d[1] = g + p;
     g = c * r - b;
-    rot_cols_c(Z, 1, c1, s1);
-    rot_cols_c(Z, 0, c, -s);
+    rot_cols_m(Z, 1, c1, s1, mir);
+    rot_cols_m(Z, 0, c, -s, mir);
     d[0] = d[0] - p;
     e[0] = g;
-}
-PCD_DEV void qr_sweep3(float d[3], float e[2], float Z[3][3]) {   // l = 2, m = 0
-    float p = d[2];
-    float g = ldiv(d[1] - p, 2.f * e[1]);
-    float r = slapy2(g, 1.f);
-    g = d[0] - p + ldiv(e[1], g + fsign(r, g));
-    float s = 1.f, c = 1.f;
-    p = 0.f;
-    float f = s * e[0], b = c * e[0];
-    slartg(g, f, c, s, r);
-    g = d[0] - p;
-    r = (d[1] - g) * s + 2.f * c * b;
-    p = s * r;
-    d[0] = g + p;
-    g = c * r - b;
-    const float c0 = c, s0 = s;
-    f = s * e[1]; b = c * e[1];
-    slartg(g, f, c, s, r);
-    e[0] = r;
-    g = d[1] - p;
-    r = (d[2] - g) * s + 2.f * c * b;
-    p = s * r;
-    d[1] = g + p;
-    g = c * r - b;
-    rot_cols_c(Z, 0, c0, s0);
-    rot_cols_c(Z, 1, c, s);
-    d[2] = d[2] - p;
-    e[1] = g;
 }
 // a 2x2 block [J, J+1] in the outer loop: deflate or slaev2 (direction only changes the deflation test's order)
 template <int J>
 PCD_DEV void block2(float d[3], float e[2], float Z[3][3]) {
     const float anorm = fmaxf(fmaxf(fmaxf(0.f, fabsf(d[J])), fabsf(d[J + 1])), fabsf(e[J]));   // NaNs drop out, as in LAPACK's loop
     if (anorm == 0.f) return;
+    const float sc = block_scale(anorm);
+    if (sc != 1.f) { d[J] *= sc; d[J + 1] *= sc; e[J] *= sc; }
     const bool qr = fabsf(d[J + 1]) < fabsf(d[J]);
     const bool small = qr ? ql_small(e[J], d[J + 1], d[J]) : ql_small(e[J], d[J], d[J + 1]);
     if (small) e[J] = 0.f;
     else tail2<J>(d, e, Z);
+    if (sc != 1.f) { const float us = block_unscale(anorm); d[J] *= us; d[J + 1] *= us; e[J] *= us; }
 }
 PCD_DEV void ssteqr3(float d[3], float e[2], float Z[3][3]) {
 #pragma unroll
@@ -293,6 +298,12 @@ PCD_DEV void ssteqr3(float d[3], float e[2], float Z[3][3]) {
         float anorm = fmaxf(fmaxf(fmaxf(0.f, fabsf(d[0])), fabsf(d[1])), fabsf(d[2]));
         anorm = fmaxf(fmaxf(anorm, fabsf(e[0])), fabsf(e[1]));
         if (anorm != 0.f) {
+            const float sc = block_scale(anorm);
+            if (sc != 1.f) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i) d[i] *= sc;
+                e[0] *= sc; e[1] *= sc;
+            }
             // LAPACK picks QL from the top, or QR from the bottom when |d[2]| < |d[0]|.  QR on (d, e, Z) is QL on the
             // reversed problem (d0 <-> d2, e0 <-> e1, Z's columns reversed) operation for operation -- the same
             // deflation tests on the same operands, the same sweep arithmetic (the rotations' sign conventions
@@ -313,7 +324,7 @@ PCD_DEV void ssteqr3(float d[3], float e[2], float Z[3][3]) {
                     if (ql_small(fe[1], fd[1], fd[2])) { fe[1] = 0.f; tail = 2; break; }
                     if (jtot == nmaxit) break;
                     ++jtot;
-                    ql_sweep3(fd, fe, Z);
+                    ql_sweep3(fd, fe, Z, qr);
                 } else {                      // l == 1: the frame's block [1,2]
                     if (ql_small(fe[1], fd[1], fd[2])) fe[1] = 0.f;
                     else tail = 1;
@@ -330,6 +341,12 @@ PCD_DEV void ssteqr3(float d[3], float e[2], float Z[3][3]) {
             }
             // the frame's [1,2] is the original [1,2] (QL) or [0,1] (QR); its [0,1] the original [0,1] or [1,2]
             if (tail != 0) tail2r((tail == 1) != qr, d, e, Z);
+            if (sc != 1.f) {
+                const float us = block_unscale(anorm);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) d[i] *= us;
+                e[0] *= us; e[1] *= us;
+            }
         }
     }
     // selection sort, ascending (swaps columns of Z)
@@ -380,6 +397,11 @@ PCD_DEV void ssteqr3_generic(float d[3], float e[2], float Z[3][3]) {
         for (int i = l; i <= lend; ++i) anorm = fmaxf(anorm, fabsf(d[i]));
         for (int i = l; i < lend; ++i) anorm = fmaxf(anorm, fabsf(e[i]));
         if (anorm == 0.f) continue;
+        const float sc = block_scale(anorm);
+        if (sc != 1.f) {
+            for (int i = l; i <= lend; ++i) d[i] *= sc;
+            for (int i = l; i < lend; ++i) e[i] *= sc;
+        }
         if (fabsf(d[lend]) < fabsf(d[l])) { lend = lsv; l = lendsv; }
         if (lend > l) {
             // ---------------- QL iteration
@@ -478,6 +500,11 @@ PCD_DEV void ssteqr3_generic(float d[3], float e[2], float Z[3][3]) {
                 e[l - 1] = g;
             }
         }
+        if (sc != 1.f) {
+            const float us = block_unscale(anorm);
+            for (int i = lsv; i <= lendsv; ++i) d[i] *= us;
+            for (int i = lsv; i < lendsv; ++i) e[i] *= us;
+        }
         if (jtot >= nmaxit) break;
     }
     // selection sort, ascending (swaps columns of Z)
@@ -505,6 +532,18 @@ PCD_DEV void eigh3(Sym3 A, float w[3], float V[3][3]) {
     return;
 #endif
     using namespace lapack;
+    // ssyevd's scaling: a matrix whose largest entry lies outside [rmin, rmax] is scaled into range first (slascl: one
+    // multiplication by sigma for every sigma reachable here) and the eigenvalues are scaled back by 1/sigma
+    const float anrm = fmaxf(fmaxf(fmaxf(fabsf(A.a00), fabsf(A.a01)), fmaxf(fabsf(A.a02), fabsf(A.a11))),
+                             fmaxf(fabsf(A.a12), fabsf(A.a22)));
+    constexpr float kRmin = 3.14018491736755e-16f;   // sqrt(slamch('S') / slamch('P')) = 2^-51.5
+    constexpr float kRmax = 3.18452583626389e+15f;   // sqrt(1 / (slamch('S') / slamch('P')))
+    float sigma = 1.f;
+    if (anrm > 0.f && anrm < kRmin) sigma = ldiv(kRmin, anrm);
+    else if (anrm > kRmax) sigma = ldiv(kRmax, anrm);
+    if (sigma != 1.f) {
+        A.a00 *= sigma; A.a01 *= sigma; A.a02 *= sigma; A.a11 *= sigma; A.a12 *= sigma; A.a22 *= sigma;
+    }
     float a22 = A.a11, a32 = A.a12, a33 = A.a22;
     const float a21 = A.a01, a31 = A.a02;
     // ssytd2 (UPLO='L'), i = 1: slarfg(2, a21, a31) -> H(1) = I - tau v vᵀ, v = (1, v2) on rows/cols 2..3
@@ -514,17 +553,17 @@ PCD_DEV void eigh3(Sym3 A, float w[3], float V[3][3]) {
         tau = ldiv(beta - a21, beta);
         v2 = a31 * ldiv(1.f, a21 - beta);
         e1 = beta;
-        // x = tau * A22 * v (ssymv, lower), w = x - tau/2 (xᵀv) v, A22 -= v wᵀ + w vᵀ (ssyr2)
-        float y1 = tau * a22;
-        float y2 = tau * a32;
-        y1 = y1 + tau * (a32 * v2);
-        y2 = y2 + (tau * v2) * a33;
+        // x = tau * A22 * v (ssymv, lower), w = x - tau/2 (xᵀv) v, A22 -= v wᵀ + w vᵀ (ssyr2), with the fma
+        // placement of MKL's kernels (fitted against mkl_lapack_ssytd2, 100 % bitwise): ssymv fuses the second column's
+        // term, the dot product does not fuse, saxpy and ssyr2 fuse every update of the trailing column
+        float y1 = fmaf(tau, a32 * v2, tau * a22);
+        float y2 = fmaf(tau * v2, a33, tau * a32);
         const float alpha = -0.5f * tau * (y1 + y2 * v2);
         y1 = y1 + alpha;
-        y2 = y2 + alpha * v2;
-        a22 = a22 - (y1 + y1);
-        a32 = a32 - (v2 * y1 + y2);
-        a33 = a33 - (v2 * y2 + y2 * v2);
+        y2 = fmaf(alpha, v2, y2);
+        a22 = (a22 - y1) - y1;
+        a32 = fmaf(v2, -y1, a32) - y2;
+        a33 = fmaf(y2, -v2, fmaf(v2, -y2, a33));
     }
     float d[3] = {A.a00, a22, a33};
     float e[2] = {e1, a32};
@@ -533,14 +572,18 @@ PCD_DEV void eigh3(Sym3 A, float w[3], float V[3][3]) {
     if (IMPL == 1) ssteqr3_generic(d, e, Z); else
 #endif
     ssteqr3(d, e, Z);
-    // sormtr: Z := H(1) Z on rows 2..3
+    // sormtr: Z := H(1) Z on rows 2..3 (slarf: w = Zᵀv unfused, then Z -= tau v wᵀ fused, as mkl_lapack_sormtr)
     if (tau != 0.f) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             const float s = Z[1][j] + v2 * Z[2][j];
-            Z[1][j] = Z[1][j] - tau * s;
-            Z[2][j] = Z[2][j] - (tau * s) * v2;
+            Z[1][j] = fmaf(-tau, s, Z[1][j]);
+            Z[2][j] = fmaf(-(tau * s), v2, Z[2][j]);
         }
+    }
+    if (sigma != 1.f) {
+        const float rs = ldiv(1.f, sigma);
+        d[0] *= rs; d[1] *= rs; d[2] *= rs;
     }
     w[0] = d[0]; w[1] = d[1]; w[2] = d[2];
 #pragma unroll
@@ -659,7 +702,8 @@ PCD_DEV Vec3 vu_smooth(const float w[3], const float V[3][3], Vec3 n, float tau,
         for (int c = 0; c < 3; ++c) acc[c] = acc[c] + mu * Er[c];
     }
     const Vec3 nn = v3(damp * n.x + acc[0], damp * n.y + acc[1], damp * n.z + acc[2]);
-    const float len = sqrtf(sq3(nn));
+    // Tensor.norm(dim=1) on the CPU accumulates the squares with fmas (x² first), then one IEEE sqrt
+    const float len = sqrtf(fmaf(nn.z, nn.z, fmaf(nn.y, nn.y, nn.x * nn.x)));
     return v3(nn.x / len, nn.y / len, nn.z / len);
 }
 

@@ -260,20 +260,37 @@ PCD_DEV Sym3 pvt_normal_cov(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, flo
 }
 
 // ----------------------------------------------------------------- H15: GraphBuilder.getPVTDecompositionWithKNN
-// C_i = Σ_j (v_j - v̄)(v_j - v̄)ᵀ with v̄ the mean of the k neighbours (GraphBuilder.py:105-110)
+// C_i = Σ_j (v_j - v̄)(v_j - v̄)ᵀ with v̄ the mean of the k neighbours (GraphBuilder.py:105-110), in torch's CPU
+// reduction order for vj.mean(dim=1) and (...).sum(dim=1) over the neighbour axis: four interleaved accumulators
+// (neighbour t into accumulator t mod 4), combined in order, the mean a division by k -- bit-identical to the
+// reference's covariances at its k = 12 (tests/test_capi.py)
 template <class P, class Nb>
 PCD_DEV Sym3 pca_cov(P pos, int cnt, Nb nb) {
-    float sx = 0.f, sy = 0.f, sz = 0.f;
-    for (int t = 0; t < cnt; ++t) { const Vec3 v = pos(nb(t)); sx += v.x; sy += v.y; sz += v.z; }
+    Vec3 s4[4] = {v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f)};
+    for (int t = 0; t < cnt; ++t) {
+        const Vec3 v = pos(nb(t));
+        Vec3& a = s4[t & 3];
+        a = t < 4 ? v : a + v;
+    }
+    Vec3 sum = s4[0];
+    for (int l = 1; l < 4 && l < cnt; ++l) sum = sum + s4[l];
     const float c = (float)cnt;
-    const Vec3 m = v3(sx / c, sy / c, sz / c);
-    Sym3 C{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const Vec3 m = v3(sum.x / c, sum.y / c, sum.z / c);
+    float C4[4][6];
     for (int t = 0; t < cnt; ++t) {
         const Vec3 d = pos(nb(t)) - m;
-        C.a00 += d.x * d.x; C.a01 += d.x * d.y; C.a02 += d.x * d.z;
-        C.a11 += d.y * d.y; C.a12 += d.y * d.z; C.a22 += d.z * d.z;
+        const float o[6] = {d.x * d.x, d.y * d.x, d.z * d.x, d.y * d.y, d.z * d.y, d.z * d.z};
+        float* a = C4[t & 3];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) a[q] = t < 4 ? o[q] : a[q] + o[q];
     }
-    return C;
+    float r[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) r[q] = cnt > 0 ? C4[0][q] : 0.f;
+    for (int l = 1; l < 4 && l < cnt; ++l)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) r[q] = r[q] + C4[l][q];
+    return Sym3{r[0], r[1], r[2], r[3], r[4], r[5]};
 }
 
 // ----------------------------------------------------------------- helpers for the position updates

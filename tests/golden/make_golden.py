@@ -11,6 +11,7 @@ Every fixture records which reference entry point produced it:
                     Selector.getKNNSelection (Selector.py:235-246), one Processor.denoise loop body at
                     k=32 staged per phase (Processor.py:119-139), iterates after 1/2/3/10 iterations in
                     fp32 and fp64, Chamfer to GT (Utils.py:253-265)
+  fandisk_k16.npz   the same at Processor.denoise()'s default k=16 (Processor.py:110)
   fandisk_denoise.npz  Processor.denoise() verbatim (k=16, 2 iterations)
   steps.npz         Denoiser.{flat,edge,feature,corner,new,dummy}_step on fixed inputs (Denoiser.py:26-232),
                     Decompositionor.getBetterFilteredNVT + Decomposition.* (Decompositionor.py:57-106,278-300)
@@ -119,7 +120,10 @@ def np32(t):
     return t.detach().cpu().numpy().astype(np.float32)
 
 
-def gen_fandisk(out_dir):
+def gen_fandisk(out_dir, k=32):
+    """fandisk_k{k}.npz: the frozen-snapshot kNN, NVT1 and one Processor.denoise loop body at feature-kNN size k
+    staged per phase, the iterates after 1/2/3/10 iterations (fp32 and fp64).  k = 32 is the metric's size; k = 16 is
+    Processor.denoise()'s own default (Processor.py:110).  The k = 32 call also writes fandisk_denoise.npz."""
     t0 = time.time()
     pos, faces = load_obj(f"{REF}/models/fandisk_gaus_n6_noisy.obj")
     gt, _ = load_obj(f"{REF}/models/fandisk.obj")
@@ -130,22 +134,22 @@ def gen_fandisk(out_dir):
     pos0 = proc.graph.pos.clone()
     res = {"pos0": np32(pos0), "n0": np32(n0), "gt": np32(gt)}
     # frozen-snapshot kNN (Selector.py:141,243) incl. scipy f64 distances
-    dist, idx = proc.selector.kdtree.query(pos0.numpy(), k=32)
-    res["knn32"] = idx.astype(np.int32)
-    res["knn32_d"] = dist.astype(np.float64)
+    dist, idx = proc.selector.kdtree.query(pos0.numpy(), k=k)
+    res[f"knn{k}"] = idx.astype(np.int32)
+    res[f"knn{k}_d"] = dist.astype(np.float64)
     sel6 = proc.selector.getKNNSelection(6)
     l = TorchUtils.averageEdgeLength(proc.graph.pos, sel6.getEdgeIndex())
     d = float(2 * l)
     res["l"] = np.float64(l)
     res["d"] = np.float64(d)
-    # Stage-by-stage NVT1 (Processor.getMyFeatureDecomposition, Processor.py:110-117) at k=32
+    # Stage-by-stage NVT1 (Processor.getMyFeatureDecomposition, Processor.py:110-117) at k
     angle = torch.pi * 5 / 12
-    sel = proc.selector.getKNNSelection(32)
+    sel = proc.selector.getKNNSelection(k)
     nvt1 = proc.decompositionor.getBetterFilteredNVT(sel, proc.graph.n, angle)
     res["eigval1"] = np32(nvt1.eigval)
     res["eigvec1"] = np32(nvt1.eigvec)
     rec = {}
-    denoise_body(proc, 32, 8, d, record=rec)
+    denoise_body(proc, k, 8, d, record=rec)
     for k_, v_ in rec.items():
         res["it1_" + k_] = v_.numpy() if v_.dtype in (torch.int64, torch.int32) else np32(v_)
     cds = [chamfer_mean(gt, pos0)]
@@ -153,7 +157,7 @@ def gen_fandisk(out_dir):
     norms = {1: np32(proc.graph.n)}
     cds.append(chamfer_mean(gt, proc.graph.pos))
     for it in range(2, 11):
-        denoise_body(proc, 32, 8, d)
+        denoise_body(proc, k, 8, d)
         cds.append(chamfer_mean(gt, proc.graph.pos))
         if it in (2, 3, 10):
             iters[it] = np32(proc.graph.pos)
@@ -167,14 +171,17 @@ def gen_fandisk(out_dir):
     p64 = Processor(pc64)
     cds64 = [chamfer_mean(gt.double(), pos0.double())]
     for it in range(1, 11):
-        denoise_body(p64, 32, 8, d)
+        denoise_body(p64, k, 8, d)
         cds64.append(chamfer_mean(gt.double(), p64.graph.pos))
         if it in (1, 2, 3, 10):
             res[f"pos64_it{it}"] = p64.graph.pos.numpy().astype(np.float64)
     res["cd_f64"] = np.asarray(cds64)
-    np.savez_compressed(os.path.join(out_dir, "fandisk_k32.npz"), **res)
-    print(f"fandisk_k32: N={N} d={d:.5f} CD {cds[0]:.4g} -> {cds[1]:.4g} {cds[2]:.4g} {cds[3]:.4g} .. {cds[-1]:.4g}"
+    res["k"] = np.int64(k)
+    np.savez_compressed(os.path.join(out_dir, f"fandisk_k{k}.npz"), **res)
+    print(f"fandisk_k{k}: N={N} d={d:.5f} CD {cds[0]:.4g} -> {cds[1]:.4g} {cds[2]:.4g} {cds[3]:.4g} .. {cds[-1]:.4g}"
           f"  ({time.time()-t0:.1f}s)")
+    if k != 32:
+        return
 
     # Processor.denoise() verbatim (k=16, k_u=8, 2 iterations)
     pc2 = Pointcloud(pos0.clone(), n0.clone())
@@ -456,7 +463,7 @@ def gen_io(out_dir):
     print(f"io: fandisk.obj V={len(v)} F={len(faces)}")
 
 
-GENS = {"fandisk": gen_fandisk, "steps": gen_steps, "lattice": gen_lattice, "mesh": gen_mesh,
+GENS = {"fandisk": gen_fandisk, "fandisk16": lambda out_dir: gen_fandisk(out_dir, 16), "steps": gen_steps, "lattice": gen_lattice, "mesh": gen_mesh,
         "metrics": gen_metrics, "cpsd": gen_cpsd, "until_min": gen_until_min, "thesis": gen_thesis, "io": gen_io}
 
 if __name__ == "__main__":

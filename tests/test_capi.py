@@ -76,43 +76,69 @@ def _t6(T):
     return np.stack([T[:, 0, 0], T[:, 1, 0], T[:, 2, 0], T[:, 1, 1], T[:, 2, 1], T[:, 2, 2]], 1)
 
 
-@pytest.mark.parametrize("which", ["nvt", "random", "pca", "degenerate"])
-def test_host_eigh_matches_torch(golden, which):
-    rng = np.random.default_rng(1)
+def _eigh_families(golden):
+    g = golden("eigh")
+    return g, sorted(k[:-2] for k in g.files if k.endswith("_T"))
+
+
+def test_host_eigh_matches_mkl_bitwise(golden):
+    """eigh3 (pcd_device.h: ssyevd = ssytd2 + ssteqr('I') + sormtr with MKL's fma placement, ssyevd's and ssteqr's
+    scaling) against torch.linalg.eigh -- the reference's own call -- BIT FOR BIT: eigenvalues and every eigenvector
+    component, on every family of tests/golden/eigh.npz (MKL 2024.2's outputs saved by make_eigh_golden.py: random,
+    rank-1 single-voter tensors whose null-space basis is set by rounding, NVT-like, PCA covariances down to 1e-6
+    spacing, matrices across the scaling bounds, repeated eigenvalues)."""
+    g, fams = _eigh_families(golden)
+    assert len(fams) >= 14
+    for fam in fams:
+        w, v = nat.host_eigh3(_t6(g[f"{fam}_T"]))
+        np.testing.assert_array_equal(w, g[f"{fam}_w"], err_msg=fam)
+        np.testing.assert_array_equal(v, g[f"{fam}_v"], err_msg=fam)
+
+
+@pytest.mark.parametrize("which", ["nvt", "pca"])
+def test_host_eigh_matches_reference_fixtures_bitwise(golden, which):
+    """The same restatement on the tensors of the reference's own runs: NVT1 of fandisk at k = 32
+    (Decompositionor.py:278-300, the fixture's eigval1 / eigvec1) and the unoriented PCA normals
+    (GraphBuilder.py:99-111, steps.npz pca_n = eigvec[..., 0])."""
     if which == "nvt":
-        T = _nvt_tensors(golden)
-    elif which == "random":
-        R = rng.standard_normal((4000, 3, 3)).astype(np.float32)
-        T = ((R + R.transpose(0, 2, 1)) / 2).astype(np.float32)
-    elif which == "pca":
+        f = golden("fandisk_k32")
+        w, v = nat.host_eigh3(_t6(_nvt_tensors(golden)))
+        np.testing.assert_array_equal(w, f["eigval1"])
+        np.testing.assert_array_equal(v, f["eigvec1"])
+    else:
         s = golden("steps")
-        vj = s["pos"][s["knn12_noself"]]
-        d = vj - vj.mean(1, keepdims=True)
-        T = (d[..., :, None] * d[..., None, :]).sum(1).astype(np.float32)
-    else:  # exact outer products of axis-aligned / lattice-like normals (repeated eigenvalues)
-        nrm = np.eye(3, dtype=np.float32)[rng.integers(0, 3, (500, 4))]
-        T = (nrm[..., :, None] * nrm[..., None, :]).mean(1).astype(np.float32)
-    w, v = nat.host_eigh3(_t6(T))
-    tw, tv = torch.linalg.eigh(torch.from_numpy(T))
-    tw, tv = tw.numpy(), tv.numpy()
-    scale = np.abs(tw).max(1, keepdims=True) + 1e-30
-    assert np.abs(w - tw).max() <= 1e-5 * scale.max() + 1e-12
-    # eigenvector signs: MKL's wherever the eigenvalue is simple.  A handful of matrices sit on a sign decision of
-    # the QL sweep (slartg's |f| > |g| test within rounding) and may flip; they are < 0.1 %.
-    gap = np.minimum(np.abs(np.diff(tw, axis=1, prepend=-np.inf)), np.abs(np.diff(tw, axis=1, append=np.inf)))
-    simple = gap > 1e-4 * scale
-    dots = (v * tv).sum(1)
-    assert (dots[simple] > 0.999).mean() >= 0.999, f"{which}: sign or vector mismatch on simple eigenvalues"
+        vj = torch.from_numpy(s["pos"])[torch.from_numpy(s["knn12_noself"].astype(np.int64))]
+        d = vj - vj.mean(dim=1)[:, None]                 # GraphBuilder.py:107-109 evaluated as written
+        T = (d[:, :, None] * d[..., None]).sum(dim=1).numpy()
+        _, v = nat.host_eigh3(_t6(T))
+        np.testing.assert_array_equal(v[..., 0], s["pca_n"])
 
 
-def test_host_vu_smooth_matches_oracle(golden):
+def test_host_vu_smooth_matches_reference_bitwise(golden):
+    """Decomposition.getVUSmoothedNormals (Decompositionor.py:92-106) on the reference's own eigen-decompositions:
+    bit-identical (Eᵀ·M·E in torch's summation order, Tensor.norm's fma accumulation)."""
     s = golden("steps")
     for rho in ("a5pi12", "api3"):
-        ev, evec, n1 = s[f"nvt_{rho}_k16_eigval"], s[f"nvt_{rho}_k16_eigvec"], s["n1"]
-        out = nat.host_vu_smooth(ev, evec, n1)
-        ref = s[f"nvt_{rho}_k16_vu"]           # the reference's own output
-        err = np.linalg.norm(out - ref, axis=1)
-        assert np.percentile(err, 99.9) < 1e-6 and err.max() < 1e-5
+        for k in (8, 16):
+            ev, evec, n1 = s[f"nvt_{rho}_k{k}_eigval"], s[f"nvt_{rho}_k{k}_eigvec"], s["n1"]
+            np.testing.assert_array_equal(nat.host_vu_smooth(ev, evec, n1), s[f"nvt_{rho}_k{k}_vu"], err_msg=(rho, k))
+
+
+@pytest.mark.parametrize("k", [8, 16])
+def test_host_nvt1_chain_matches_reference_bitwise(golden, k):
+    """The fused kernels' NVT1 (vote + list-order tensor sums, eigh3, VU smoothing) on the host against the
+    reference's getBetterFilteredNVT + getVUSmoothedNormals outputs (steps.npz): every eigenvalue, eigenvector and
+    smoothed normal bit-identical, single-voter neighbourhoods included."""
+    s = golden("steps")
+    pos, n1 = s["pos"], s["n1"]
+    knn = s[f"knn{k}"].astype(np.int64)
+    m = len(knn)
+    for rho_name, rho in (("a5pi12", math.pi * 5 / 12), ("api3", math.pi / 3)):
+        t6 = nat.host_nvt_tensor(pos, n1, np.arange(m), np.arange(m + 1) * k, knn.reshape(-1), rho)
+        w, v = nat.host_eigh3(t6)
+        np.testing.assert_array_equal(w, s[f"nvt_{rho_name}_k{k}_eigval"])
+        np.testing.assert_array_equal(v, s[f"nvt_{rho_name}_k{k}_eigvec"])
+        np.testing.assert_array_equal(nat.host_vu_smooth(w, v, n1), s[f"nvt_{rho_name}_k{k}_vu"])
 
 
 def test_host_solve3():
