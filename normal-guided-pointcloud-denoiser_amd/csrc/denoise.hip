@@ -976,7 +976,7 @@ __global__ __launch_bounds__(256) void k_class_rows_maxdist(const float4* __rest
             if (!on[r]) continue;
 #pragma unroll
             for (int u = 0; u < KU; ++u)
-                if (u < ku) mx2 = fmaxf(mx2, sq3(v3(v[r][u].x, v[r][u].y, v[r][u].z) - ctr));
+                if (u < ku) mx2 = fmaxf(mx2, nsq3(v3(v[r][u].x, v[r][u].y, v[r][u].z) - ctr));
         }
     }
     float mx = sqrtf(mx2);
@@ -1057,7 +1057,7 @@ __global__ __launch_bounds__(256, PCD_PHASE_OCC) void k_phase(const float4* __re
     else o = vi;
     if (clampg > 0.f) {                 // global clamp against the loaded positions (PostProcessing.ipynb:1088-1089)
         const float4 o4 = orig[i];
-        const bool keep = sqrtf(sq3(o - v3(o4.x, o4.y, o4.z))) < clampg;
+        const bool keep = norm3(o - v3(o4.x, o4.y, o4.z)) < clampg;
         o = sel3(keep, o, vi);
     }
     store4(pout, i, o);

@@ -172,7 +172,7 @@ __global__ void k_rows_maxdist(Rows3 pos, const int64_t* __restrict__ nbr, int64
     const Vec3 c = v3(g[0], g[1], g[2]);
     float mx = 0.f;
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < e; t += (int64_t)gridDim.x * blockDim.x)
-        mx = fmaxf(mx, sqrtf(sq3(pos(nbr[t]) - c)));
+        mx = fmaxf(mx, norm3(pos(nbr[t]) - c));
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
     if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(g) + 3, __float_as_uint(mx));
 }
@@ -203,7 +203,7 @@ __global__ void k_edge_len(Rows3 pos, const int64_t* __restrict__ a, const int64
                            double* __restrict__ sum) {
     double acc = 0;
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < e; t += (int64_t)gridDim.x * blockDim.x)
-        acc += (double)sqrtf(sq3(pos(b[t]) - pos(a[t])));
+        acc += (double)norm3(pos(b[t]) - pos(a[t]));
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if ((threadIdx.x & 63) == 0) atomicAdd(sum, acc);
 }

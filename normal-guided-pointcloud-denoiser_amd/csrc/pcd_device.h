@@ -26,6 +26,11 @@ PCD_DEV Vec3 operator*(float s, Vec3 a) { return v3(s * a.x, s * a.y, s * a.z); 
 // dot in the reference's summation order: (x*x' + y*y') + z*z'  ((a*b).sum(dim=1))
 PCD_DEV float dot3(Vec3 a, Vec3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }  // built with -ffp-contract=off
 PCD_DEV float sq3(Vec3 a) { return dot3(a, a); }
+// Tensor.norm(dim=1) / F.normalize as torch computes them on the CPU: the squares accumulated with fmas (x² first),
+// then one IEEE sqrt -- every ||.|| the reference compares against a threshold (the step clamps, the global clamp,
+// flat_step's delta, the vote's normalize) rounds this way (pinned in oracle.norm3 against torch)
+PCD_DEV float nsq3(Vec3 a) { return fmaf(a.z, a.z, fmaf(a.y, a.y, a.x * a.x)); }   // the sum under norm3's root
+PCD_DEV float norm3(Vec3 a) { return sqrtf(nsq3(a)); }
 // c ? a : b component by component (a select of the structs themselves can leave them in scratch memory)
 PCD_DEV Vec3 sel3(bool c, Vec3 a, Vec3 b) { return v3(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
 

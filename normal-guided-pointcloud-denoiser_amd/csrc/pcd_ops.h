@@ -103,7 +103,7 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF n
         const bool near = sq != 0.f && (!(fabsf(lhs - rhs) > m) || !(sq >= 1e-24f && sq < 1e30f));
         bool w = sq == 0.f ? w_self : lhs < rhs;
         if (near) {
-            const float den = fmaxf(sqrtf(sq), 1e-12f);
+            const float den = fmaxf(norm3(v3(dxy.x, dxy.y, dz)), 1e-12f);
             const Vec3 dn = v3(dxy.x / den, dxy.y / den, dz / den);
             float c = dot3(dn, nj);
             c = fabsf(fminf(fmaxf(c, -1.f), 1.f));
@@ -309,7 +309,7 @@ PCD_DEV void add_outer(float A[3][3], Vec3 a, float s = 1.f) {
 // di = α(x - v_i); accept if ||di|| < d (strict; flat_step uses <=)
 PCD_DEV Vec3 clamp_step(Vec3 vi, Vec3 x, float alpha, float d) {
     const Vec3 di = v3((x.x - vi.x) * alpha, (x.y - vi.y) * alpha, (x.z - vi.z) * alpha);
-    const float nrm = sqrtf(sq3(di));
+    const float nrm = norm3(di);
     return sel3(nrm < d, vi + di, vi);
 }
 
@@ -329,7 +329,7 @@ PCD_DEV Vec3 step_flat(P pos, Nr nrm, Vec3 vi, Vec3 ni, int cnt, Nb nb, float de
         ws += W;
     });
     const Vec3 di = v3(sx / ws * alpha, sy / ws * alpha, sz / ws * alpha);
-    const float nrm2 = sqrtf(sq3(di));
+    const float nrm2 = norm3(di);
     return sel3(nrm2 <= d, vi + di, vi);   // NaN (Σ W = 0) -> no move, as di[~mask] = 0
 }
 

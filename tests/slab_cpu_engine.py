@@ -76,7 +76,7 @@ class CpuSlabEngine:
         elif stage == nat.STAGE_PHASE_MAXDIST:
             rows = self._class_rows(params, phase)
             vj = self.pos[self.idx[rows, :ku]].reshape(-1, 3)
-            m = np.sqrt(((vj - self.centre[phase]) ** 2).sum(1)).max() if len(vj) else F32(0)
+            m = O.norm3(vj - self.centre[phase]).max() if len(vj) else F32(0)
             red.copy_(torch.tensor([float(m)], dtype=torch.float32))
         elif stage == nat.STAGE_PHASE_APPLY:
             rows = self._class_rows(params, phase)

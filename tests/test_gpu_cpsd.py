@@ -1,9 +1,10 @@
 """GPU parity of the CPSD ("Martin") feature path: radius selection, normal-filtered NVT / PVT, VU
 features, against the reference's golden vectors (tests/golden/cpsd.npz, make_golden.py gen_cpsd) and the oracle.
 
-Tolerances: radius selections identical (same float64 membership test as scipy); eigenvalues <= 2e-6 abs (NVT) /
-1e-5 relative (PVT, on rows whose smoothed normals agree); smoothed normals median 0 and >= 99.8 % within 1e-4 rad;
-VU classes >= 99.5 % identical (a class flips only where an eigenvalue sits within rounding of tau).
+Tolerances: radius selections identical (same float64 membership test as scipy); the normal-filtered NVT, VU
+smoothing, the normal-filtered PVT and the VU classes bit-identical to the reference's (sums in the reference's order,
+the MKL-exact eigh); the corner step bit-identical on the reference's inputs; the driver's first iteration median 0,
+p99 <= 1e-8 x bbox (the flat step's exp() and float32 global mean are the only operations not restated to the bit).
 """
 import math
 
@@ -81,27 +82,26 @@ def test_radius_selection_edge_cases(proc, gpu):
 
 def test_martin_feature_decomposition(cpsd, proc):
     dec, fn = proc.getMartinFeatureDecomposition(r=float(cpsd["d"]))
-    ang = angle64(fn.cpu().numpy(), cpsd["f_n"])
-    assert np.median(ang) < 1e-6 and (ang < 1e-4).mean() >= 0.998, np.percentile(ang, [50, 99, 100])
-    # end to end against the reference: a vote can flip where a neighbour's f_n differs in the last bits
-    ref = cpsd["pvt_eigval"]
-    scale = np.abs(ref).max(1, keepdims=True) + 1e-30
-    err = (np.abs(dec.eigval.cpu().numpy() - ref) / scale).max(1)
-    assert (err < 1e-5).mean() >= 0.995 and np.median(err) < 1e-6, ((err < 1e-5).mean(), np.median(err))
-    agree = (dec.getVUFeatures(tau=0.3).cpu().numpy() == cpsd["vu_classes"]).mean()
-    assert agree >= 0.995, agree
-    # the PVT kernel alone, fed the GPU's own f_n: the oracle on identical inputs
+    fn, w, v = fn.cpu().numpy(), dec.eigval.cpu().numpy(), dec.eigvec.cpu().numpy()
+    report(f"martin: f_n exact {(fn == cpsd['f_n']).all(1).mean():.6f}, PVT eigval exact "
+           f"{(w == cpsd['pvt_eigval']).all(1).mean():.6f}, eigvec exact {(v == cpsd['pvt_eigvec']).all((1, 2)).mean():.6f}")
+    np.testing.assert_array_equal(fn, cpsd["f_n"])
+    np.testing.assert_array_equal(w, cpsd["pvt_eigval"])
+    np.testing.assert_array_equal(v, cpsd["pvt_eigvec"])
+    np.testing.assert_array_equal(dec.getVUFeatures(tau=0.3).cpu().numpy(), cpsd["vu_classes"])
+    # the PVT kernel alone, fed the GPU's own f_n: the oracle on identical inputs, bit for bit
     pos = cpsd["pos"]
     slices, j = O.radius_selection(pos, pos, float(cpsd["d"]))
-    w_ref, _ = O.normal_filtered_pvt(pos, fn.cpu().numpy(), np.arange(len(pos)), slices, j, 0.9)
-    e2 = (np.abs(dec.eigval.cpu().numpy() - w_ref) / (np.abs(w_ref).max(1, keepdims=True) + 1e-30)).max(1)
-    assert (e2 < 1e-5).mean() >= 0.999 and np.median(e2) < 1e-6, ((e2 < 1e-5).mean(), np.median(e2))
+    w_ref, v_ref = O.normal_filtered_pvt(pos, fn, np.arange(len(pos)), slices, j, 0.9)
+    np.testing.assert_array_equal(w, w_ref)
+    np.testing.assert_array_equal(v, v_ref)
 
 
 def test_normal_filtered_nvt(cpsd, proc):
     sel = proc.selector.getPointsInRangeSelection(float(cpsd["d"]))
     nvt = proc.decompositionor.getNormalFilteredNVT(sel, proc.graph.n, 0.9)
-    np.testing.assert_allclose(nvt.eigval.cpu().numpy(), cpsd["nvt_eigval"], atol=2e-6)
+    np.testing.assert_array_equal(nvt.eigval.cpu().numpy(), cpsd["nvt_eigval"])
+    np.testing.assert_array_equal(nvt.eigvec.cpu().numpy(), cpsd["nvt_eigvec"])
 
 
 def test_vu_decomposition(cpsd, proc):
@@ -109,6 +109,9 @@ def test_vu_decomposition(cpsd, proc):
     ref = cpsd["vud_eigval"]
     scale = np.abs(ref).max(1, keepdims=True) + 1e-30
     err = np.abs(vu.eigval.cpu().numpy() - ref) / scale
+    # the radius is 2 x the mean kNN(6) edge length, an f64 mean here and a float32 torch mean there, so a member
+    # at the boundary can differ: reported, gated on the eigenvalues
+    report(f"VU decomposition: eigval exact {(err == 0).all(1).mean():.6f}, max rel {err.max():.3g}")
     assert np.percentile(err, 99) < 1e-5 and np.median(err) < 1e-6, np.percentile(err, [50, 99, 100])
 
 
@@ -134,10 +137,12 @@ def test_cpsd_corner_step(cpsd, proc):
     corners = torch.as_tensor(cpsd["corner_idx"], device=proc.graph.pos.device)
     sel8 = proc.selector.getKNNSelection(8)
     out = proc.denoiser.corner_step(sel8.filter(corners), T(cpsd["f_n"], proc.graph.pos.device),
-                                    float(cpsd["d"]) * 20000, 1.0)
+                                    float(cpsd["d"]) * 20000, 1.0).cpu().numpy()
     bbox = np.linalg.norm(cpsd["pos"].max(0) - cpsd["pos"].min(0))
-    dev = np.linalg.norm(out.cpu().numpy() - cpsd["corner_pos"], axis=1) / bbox
-    assert np.median(dev) < 1e-6 and np.percentile(dev, 99) < 1e-4, np.percentile(dev, [50, 99, 100])
+    dev = np.linalg.norm(out - cpsd["corner_pos"], axis=1) / bbox
+    report(f"cpsd corner step: exact {(dev == 0).mean():.4f} max {dev.max():.3g} over {len(dev)} corners")
+    # inv_ex + einsum restated operation for operation, the sums in list order: the reference's output bit for bit
+    np.testing.assert_array_equal(out, cpsd["corner_pos"])
 
 
 def test_cpsd_driver_matches_reference(cpsd, gpu):
@@ -156,15 +161,15 @@ def test_cpsd_driver_matches_reference(cpsd, gpu):
         dev = np.linalg.norm(v.cpu().numpy() - ref, axis=1) / bbox
         report(f"cpsd driver it{it}: exact {np.mean(dev == 0):.4f} median {np.median(dev):.3g} "
               f"p99 {np.percentile(dev, 99):.3g} max {dev.max():.3g}")
+        # n := f_n (radius NVT + VU smoothing): bit-identical to the reference's, iteration after iteration
+        np.testing.assert_array_equal(proc.graph.n.cpu().numpy(), cpsd[f"drv_n_it{it}"])
         if it == 1:
-            # the CPSD path's f32 eigen-solves (normal-filtered NVT / PVT, LAPACK-restated vs MKL ssyevd) differ from
-            # the reference's by ~1e-7 relative (test_martin_feature_decomposition, test_vu_decomposition), which the
-            # steps carry into the positions: measured median 4.9e-7, p99 1.8e-5 x bbox (r5a)
-            assert np.median(dev) <= 1e-6 and np.percentile(dev, 99) <= 5e-5, (np.median(dev), np.percentile(dev, 99))
-            nd = np.abs(proc.graph.n.cpu().numpy() - cpsd["drv_n_it1"]).max(1)
-            assert np.percentile(nd, 99) < 1e-5, np.percentile(nd, 99)
+            # (round 5, before the MKL-exact eigh: median 4.9e-7, p99 1.8e-5 -- the eigen-solves' last bits); now
+            # only the flat step's exp() / global centre differ: measured exact on 99.9 % of the rows, max 1.8e-10
+            assert np.median(dev) == 0 and np.percentile(dev, 99) <= 1e-8 and dev.max() <= 1e-6, \
+                (np.median(dev), np.percentile(dev, 99), dev.max())
         else:
-            assert np.median(dev) < 1e-5 and np.percentile(dev, 99) < 5e-3, (np.median(dev), np.percentile(dev, 99))
+            assert np.median(dev) == 0 and np.percentile(dev, 99) <= 1e-6, (np.median(dev), np.percentile(dev, 99))
         assert proc.graph.pos is v                                   # updated in place
         moved = np.linalg.norm(v.cpu().numpy() - pos0, axis=1)
         assert moved.max() < d                                        # the global clamp (ipynb:1060-1061)

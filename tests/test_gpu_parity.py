@@ -1,9 +1,11 @@
 """GPU parity: the HIP path (through libpcd's C-ABI and the drop-in classes) against the reference's golden vectors
 and the CPU oracle.  Run on an MI355X with `pytest -m gpu`.
 
-Tolerances (fp32): kNN sets identical except distance near-ties; eigenvalues <= 2e-6 abs;
-smoothed normals <= 1e-4 rad except near a threshold; classes identical except near-margin points (>= 99.8 %);
-positions p99 <= 1e-5 x bbox for one step; multi-iteration runs within the reference's own fp32-vs-fp64 envelope.
+Tolerances (fp32): kNN sets identical except distance near-ties; NVT1 (vote, list-order sums, the
+MKL-exact eigh, VU smoothing) and the solve steps (edge / feature / corner) bit-identical to the reference's outputs
+on the same inputs; the flat / new steps (torch's vectorised exp and float32 global mean are the only operations not
+restated to the bit) within 1e-6 x bbox; one iteration end to end p99 <= 1e-6 x bbox; multi-iteration runs within
+the reference's own fp32-vs-fp64 envelope (the loop is chaotic).
 """
 import math
 
@@ -192,25 +194,13 @@ def test_nvt_decomposition(steps, gpu, rho, k):
     sel = Selection(torch.arange(m, device=gpu), knn.reshape(-1), torch.arange(m + 1, device=gpu) * k)
     r = ANGLE if rho == "a5pi12" else math.pi / 3
     dec = Decompositionor(g).getBetterFilteredNVT(sel, n1, r)
-    ev = dec.eigval.cpu().numpy()
-    np.testing.assert_allclose(ev, steps[f"nvt_{rho}_k{k}_eigval"], atol=2e-6)
-    cls = dec.getClasses().cpu().numpy()
-    assert (cls == steps[f"nvt_{rho}_k{k}_classes"]).mean() >= 0.999
-    vu = dec.getVUSmoothedNormals(n1).cpu().numpy()
-    a = angle(vu, steps[f"nvt_{rho}_k{k}_vu"])
-    # VU smoothing uses Eᵀ·M·E (not the projector), so it depends on eigenvector SIGNS and, for exactly degenerate
-    # tensors (a single voting neighbour: T = n nᵀ), on the basis LAPACK picks in the null space.  Those are
-    # rounding-level decisions of MKL's ssyevd; a small fraction of points lands on them (parity).
-    # Single-voter neighbourhoods give T = n nᵀ exactly: the two null-space eigenvectors are set by ~1e-8 rounding
-    # noise (MKL's FMA code path vs ours), and Eᵀ·M·E reads row 0 of that basis, so there the reference's own output
-    # is not reproducible across CPUs.  Strict bar on every other point; the degenerate ones are only counted.
-    vj = steps["pos"][steps[f"knn{k}"]] - steps["pos"][:, None, :]
-    dn = vj / np.maximum(np.linalg.norm(vj, axis=-1, keepdims=True), 1e-12)
-    c = np.abs(np.clip((dn * steps["n1"][steps[f"knn{k}"]]).sum(-1), -1, 1))
-    voters = (np.arccos(c) > np.float32(r)).sum(1)
-    degenerate = voters == 1
-    assert np.median(a) < 1e-6
-    assert (a[~degenerate] > 1e-3).mean() < 0.002, (a[~degenerate] > 1e-3).mean()
+    # the vote, the tensor sums in list order and the MKL-exact eigh (pcd_device.h eigh3): the reference's
+    # eigenvalues AND eigenvectors bit for bit -- single-voter (rank-1) tensors, whose null-space basis is set by
+    # rounding, included -- so VU smoothing (Eᵀ·M·E, sign-dependent) is bit-identical too
+    np.testing.assert_array_equal(dec.eigval.cpu().numpy(), steps[f"nvt_{rho}_k{k}_eigval"])
+    np.testing.assert_array_equal(dec.eigvec.cpu().numpy(), steps[f"nvt_{rho}_k{k}_eigvec"])
+    np.testing.assert_array_equal(dec.getClasses().cpu().numpy(), steps[f"nvt_{rho}_k{k}_classes"])
+    np.testing.assert_array_equal(dec.getVUSmoothedNormals(n1).cpu().numpy(), steps[f"nvt_{rho}_k{k}_vu"])
     pl, li, sp = dec.getNVTFeatures()
     feats = torch.stack([pl, li, sp], 1).cpu().numpy()
     np.testing.assert_allclose(feats, steps[f"nvt_{rho}_k{k}_features"], rtol=1e-4, atol=2e-5)
@@ -238,9 +228,20 @@ def test_denoiser_steps(steps, gpu, kind, alpha):
             out = den.edge_step(s, n1, ev, dd, alpha)
         else:
             out = getattr(den, f"{kind}_step")(s, n1, dd, alpha)
-        dev = np.linalg.norm(out.cpu().numpy() - steps[key], axis=1) / bbox
-        assert np.percentile(dev, 95) < 1e-5, (key, np.percentile(dev, 95))
-        assert (dev < 1e-3).mean() > 0.99, key
+        out = out.cpu().numpy()
+        dev = np.linalg.norm(out - steps[key], axis=1) / bbox
+        report(f"step {key}: exact {(dev == 0).mean():.4f} p99.9 {np.percentile(dev, 99.9):.3g} max {dev.max():.3g}")
+        if kind in ("edge", "feature", "corner", "dummy"):
+            # torch's inv_ex (MKL getrf(Aᵀ) + getrs('T')) and einsum restated operation for operation, the sums in
+            # list order: the reference's own output, every row
+            np.testing.assert_array_equal(out, steps[key], err_msg=key)
+        else:
+            # flat / new: exp() (torch's vectorised exp rounds differently in ~10 % of arguments, by 1 ulp) and the
+            # global centre (a float32 torch mean here, an f64 mean reduced on the device) -- no row excluded.  The
+            # new step's weights scale its 3x3 system (unnormalised), so a 1-ulp weight moves the solve further:
+            # measured flat max 1.8e-7, new p99.9 1.2e-6 / max 3.2e-6 (83 % of its rows exact)
+            tol = (1e-6, 2e-6) if kind == "flat" else (2e-6, 6e-6)
+            assert np.percentile(dev, 99.9) <= tol[0] and dev.max() <= tol[1], (key, np.percentile(dev, 99.9), dev.max())
 
 
 def test_steps_on_filtered_csr_selection(steps, gpu):
@@ -267,10 +268,8 @@ def test_pca_normals_and_orientation(steps, golden, gpu):
     ei = torch.stack([torch.arange(len(pos), device=gpu).repeat_interleave(12),
                       T(steps["knn12_noself"].astype(np.int64), gpu).reshape(-1)])
     ev = gb.getPVTDecompositionWithKNN(ei)[..., 0].cpu().numpy()
-    ref = steps["pca_n"]
-    dots = (ev * ref).sum(1) / np.linalg.norm(ev, axis=1) / np.linalg.norm(ref, axis=1)
-    assert (np.abs(dots) > 0.9999).mean() > 0.999
-    assert (dots > 0).mean() > 0.995                          # LAPACK sign convention reproduced
+    # covariances in torch's reduction order, the MKL-exact eigh: the reference's unoriented normals bit for bit
+    np.testing.assert_array_equal(ev, steps["pca_n"])
     # full setAndFlipNormals on the fandisk input reproduces the reference's oriented normals
     fan = golden("fandisk_k32")
     gb2 = GraphBuilder(Pointcloud(T(fan["pos0"], gpu)))
@@ -295,15 +294,26 @@ def _fused(fan, gpu, iterations, k=32, k_u=8):
     return pos.cpu().numpy(), n.cpu().numpy(), cls.cpu().numpy()
 
 
-def test_fused_iteration_matches_reference(fan, gpu):
-    pos, n, cls = _fused(fan, gpu, 1)
-    assert (cls == fan["it1_classes"]).mean() >= 0.998
-    a = angle(n, fan["it1_f_n"])
-    assert np.percentile(a, 99) < 1e-4 and (a < 1e-2).mean() > 0.998
-    bbox = np.linalg.norm(fan["pos0"].max(0) - fan["pos0"].min(0))
-    dev = np.linalg.norm(pos - fan["it1_pos_after_2"], axis=1) / bbox
-    report(f"fandisk 1 iteration: median {np.median(dev):.3g} p99 {np.percentile(dev, 99):.3g} max {dev.max():.3g}")
-    assert np.percentile(dev, 99) <= 1e-5 and np.median(dev) <= 1e-7
+@pytest.mark.parametrize("k", [32, 16])
+def test_fused_iteration_matches_reference(golden, gpu, k):
+    """One fused iteration (kNN + NVT1 + NVT2 + the Gauss-Seidel phases) against the reference's loop body at k = 32
+    and at Processor.denoise()'s default k = 16: f_n (NVT1) and the classes bit-identical, positions p99 <= 1e-6,
+    max <= 1e-5 x bbox (the flat step's exp / centre rounding carried through the chained edge and feature solves)."""
+    f = golden(f"fandisk_k{k}")
+    pos, n, cls = _fused(f, gpu, 1, k=k)
+    np.testing.assert_array_equal(n, f["it1_f_n"])
+    np.testing.assert_array_equal(cls, f["it1_classes"])
+    bbox = np.linalg.norm(f["pos0"].max(0) - f["pos0"].min(0))
+    dev = np.linalg.norm(pos - f["it1_pos_after_2"], axis=1) / bbox
+    report(f"fandisk k={k} 1 iteration: exact {(dev == 0).mean():.4f} median {np.median(dev):.3g} "
+           f"p99 {np.percentile(dev, 99):.3g} max {dev.max():.3g}")
+    assert np.median(dev) == 0 and np.percentile(dev, 99) <= 1e-6 and dev.max() <= 1e-5
+    # iteration 2 on the loop's own state: the chaotic envelope (SURVEY §8(c)), reported
+    pos2, _, _ = _fused(f, gpu, 2, k=k)
+    dev2 = np.linalg.norm(pos2 - f["pos_it2"], axis=1) / bbox
+    report(f"fandisk k={k} 2 iterations: exact {(dev2 == 0).mean():.4f} median {np.median(dev2):.3g} "
+           f"p99 {np.percentile(dev2, 99):.3g} max {dev2.max():.3g}")
+    assert np.median(dev2) <= 1e-7 and np.percentile(dev2, 99) <= 1e-4
 
 
 @pytest.mark.parametrize("k,anchoring", [(8, True), (16, True), (32, True), (64, True), (16, False), (32, False)])
@@ -400,18 +410,31 @@ def test_fused_ten_iterations_cd_envelope(fan, gpu):
 
 
 def test_processor_denoise_verbatim(golden, gpu):
-    """Processor.denoise() with its defaults (k=16, k_u=8, 2 iterations, d=2l), aliasing included."""
+    """Processor.denoise() with its defaults (k=16, k_u=8, 2 iterations, d=2l), aliasing included: after ONE iteration
+    against the reference's k = 16 loop body (fandisk_k16: n = f_n bit-identical, positions p99 <= 1e-6 x bbox), after
+    the default two against the reference's own Processor.denoise() run (fandisk_denoise)."""
+    f16 = golden("fandisk_k16")
+    v1 = T(f16["pos0"], gpu).clone()
+    p1 = Processor(Pointcloud(v1, T(f16["n0"], gpu).clone()))
+    p1.denoise(iterations=1)
+    bbox = np.linalg.norm(f16["pos0"].max(0) - f16["pos0"].min(0))
+    np.testing.assert_array_equal(p1.graph.n.cpu().numpy(), f16["n_it1"])
+    dev1 = np.linalg.norm(v1.cpu().numpy() - f16["pos_it1"], axis=1) / bbox
+    report(f"Processor.denoise() 1 iteration: exact {(dev1 == 0).mean():.4f} median {np.median(dev1):.3g} "
+           f"p99 {np.percentile(dev1, 99):.3g} max {dev1.max():.3g}")
+    assert np.median(dev1) == 0 and np.percentile(dev1, 99) <= 1e-6 and dev1.max() <= 1e-5
     g = golden("fandisk_denoise")
     v = T(g["pos0"], gpu).clone()
     pc = Pointcloud(v, T(g["n0"], gpu).clone())
     proc = Processor(pc)
     proc.denoise()
     assert proc.graph.pos is v and pc.v is v                 # graph.pos mutated in place (GraphBuilder.py:50)
-    bbox = np.linalg.norm(g["pos0"].max(0) - g["pos0"].min(0))
     dev = np.linalg.norm(v.cpu().numpy() - g["pos"], axis=1) / bbox
-    assert np.percentile(dev, 99) < 5e-3 and np.median(dev) < 1e-5
+    report(f"Processor.denoise() 2 iterations: exact {(dev == 0).mean():.4f} median {np.median(dev):.3g} "
+           f"p99 {np.percentile(dev, 99):.3g} max {dev.max():.3g}")
+    assert np.median(dev) <= 1e-7 and np.percentile(dev, 99) <= 1e-4
     a = angle(proc.graph.n.cpu().numpy(), g["n"])
-    assert np.median(a) < 1e-5
+    assert np.median(a) < 1e-6
 
 
 def test_processor_on_cpu_tensors_returns_cpu(golden, gpu):
@@ -476,16 +499,22 @@ def test_thesis_driver_matches_reference(golden, gpu):
     proc = Processor(pc)
     proc.thesisDenoise(iterations=1, d=float(g["d"]))
     bbox = np.linalg.norm(g["pos0"].max(0) - g["pos0"].min(0))
+    # f_n at the driver's k = 16 (getMyFeatureDecomposition's default): bit-identical
+    np.testing.assert_array_equal(proc.graph.n.cpu().numpy(), g["n_it1"])
     dev1 = np.linalg.norm(v.cpu().numpy() - g["pos_it1"], axis=1) / bbox
-    report(f"thesis 1 iteration: median {np.median(dev1):.3g} p99 {np.percentile(dev1, 99):.3g} max {dev1.max():.3g}")
-    # (r5b: median 0, p99 1.9e-4, max 5.9e-3 x bbox: the thesis cloud's few discrete decisions -- classes, the
-    # per-step clamp -- that round differently; the NVT path's own one-iteration gate is test_fused_iteration_matches_
-    # reference's 1e-5)
-    assert np.percentile(dev1, 99) <= 3e-4 and np.median(dev1) <= 1e-7
+    rejected = ~g["mask_it1"]
+    report(f"thesis 1 iteration: exact {(dev1 == 0).mean():.4f} median {np.median(dev1):.3g} "
+           f"p99 {np.percentile(dev1, 99):.3g} max {dev1.max():.3g}; {int(rejected.sum())} rows held by the global clamp")
+    # (round 5, before the MKL-exact eigh: p99 1.9e-4, max 5.9e-3 -- VU smoothing's eigenvector signs at k = 16)
+    # the rows the reference's global clamp held keep their input positions here too
+    np.testing.assert_array_equal(v.cpu().numpy()[rejected], g["pos0"][rejected])
+    assert np.median(dev1) == 0 and np.percentile(dev1, 99) <= 1e-6 and dev1.max() <= 1e-5
     proc2 = Processor(Pointcloud(T(g["pos0"], gpu).clone(), T(g["n0"], gpu).clone()))
     proc2.thesisDenoise(iterations=2, d=float(g["d"]))
     dev2 = np.linalg.norm(proc2.graph.pos.cpu().numpy() - g["pos_it2"], axis=1) / bbox
-    assert np.percentile(dev2, 99) < 5e-3 and np.median(dev2) < 1e-5
+    report(f"thesis 2 iterations: exact {(dev2 == 0).mean():.4f} median {np.median(dev2):.3g} "
+           f"p99 {np.percentile(dev2, 99):.3g} max {dev2.max():.3g}")
+    assert np.median(dev2) <= 1e-7 and np.percentile(dev2, 99) <= 1e-4
     # the global clamp: no point ends farther than d from where it started
     moved = np.linalg.norm(proc2.graph.pos.cpu().numpy() - g["pos0"], axis=1)
     assert moved.max() < float(g["d"])

@@ -124,9 +124,12 @@ def _one_iteration_vs_oracle(pos, nrm, k, dev):
     dev_pos = np.linalg.norm(gp.cpu().numpy() - rpos, axis=1) / bbox
     report(f"{N} points, 1 iteration vs the oracle: classes {agree:.6f} median {np.median(dev_pos):.3g} "
           f"p99 {np.percentile(dev_pos, 99):.3g} p99.9 {np.percentile(dev_pos, 99.9):.3g} max {dev_pos.max():.3g}")
-    assert agree >= 0.998, agree
-    assert np.percentile(dev_pos, 99) <= 1e-5 and np.median(dev_pos) <= 1e-7, (np.percentile(dev_pos, 99),
-                                                                              np.median(dev_pos))
+    # the oracle restates NVT1 to the bit (MKL-exact eigh, torch's norm), so only kNN near-ties between the fp32 grid
+    # and the f64 KD-tree, NVT2's Jacobi at an argmax margin and the flat step's exp / centre rounding remain
+    # (measured at 170k / 200k / 1M: classes >= 0.999999, median 0, p99 <= 5.1e-8, p99.9 <= 2.0e-7)
+    assert agree >= 0.99999, agree
+    assert np.median(dev_pos) == 0 and np.percentile(dev_pos, 99) <= 1e-6 and np.percentile(dev_pos, 99.9) <= 1e-5, \
+        (np.median(dev_pos), np.percentile(dev_pos, 99), np.percentile(dev_pos, 99.9))
 
 
 def test_headline_workload_sample_one_iteration_vs_oracle(gpu):

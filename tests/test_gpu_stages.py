@@ -108,10 +108,11 @@ def check_stages(got, ref_cls, ref_fn, ref_eig2, ref_edge, ref_after, knn, pos0,
         assert fn_same.all(), label                                # (the injected field, round trip exact)
     nb_fn_ok = fn_ok[knn[:, :k]].all(1) & fn_ok
     excl = 1 - nb_fn_ok.mean()
-    # own f_n: K1's smoothed normals differ from the reference's beyond 1e-5 rad on ~0.1-0.3 % of the points (VU
-    # smoothing's sign / near-degenerate eigenvector cases, test_gpu_parity); with k = 32 neighbours each, that
-    # excludes a few % of the neighbourhoods from the NVT2 comparison
-    assert excl < (1e-9 if injected else 0.10), f"{label}: {excl:.4f} of the points have a neighbour whose f_n differs"
+    # own f_n: K1's smoothed normals are the reference's bit for bit wherever its kNN list is (the MKL-exact eigh,
+    # test_fused_stages_match_reference_fixture); only rows whose fp32 grid list orders a near-tie differently from
+    # the reference's f64 KD-tree can differ (measured: no neighbourhood excluded on fandisk or the 200k sample;
+    # round 5, before the MKL-exact eigh: 2.4-7.5 %)
+    assert excl < (1e-9 if injected else 0.005), f"{label}: {excl:.4f} of the points have a neighbour whose f_n differs"
     # NVT2 eigenvalues: the reference normalises T by Σw before eigh; the kernel divides its eigenvalues by Σw
     e = np.abs(got["eig2"][:, :3] - ref_eig2)[nb_fn_ok]
     assert e.max() <= 2e-6, f"{label}: NVT2 eigenvalue error max {e.max():.3g} (p99.9 {np.percentile(e, 99.9):.3g})"
@@ -179,8 +180,8 @@ def check_stages(got, ref_cls, ref_fn, ref_eig2, ref_edge, ref_after, knn, pos0,
             assert stats[ph][2] <= 1e-6 and stats[ph][3] < 0.02, (label, ph, stats[ph])
         else:
             assert stats[ph][1] <= 2e-6 and stats[ph][2] <= 3e-6, (label, ph, stats[ph])
-            assert stats[ph][3] <= 0.10, (label, ph, stats[ph])
-    assert dec_ok.mean() > (0.99 if injected else 0.90), (label, dec_ok.mean())
+            assert stats[ph][3] <= 0.01, (label, ph, stats[ph])
+    assert dec_ok.mean() > 0.99, (label, dec_ok.mean())
     return stats
 
 
@@ -262,7 +263,9 @@ def test_nvt2_jacobi_matches_lapack_restatement(gpu):
     w0, V0, w1, y1 = w0.cpu().numpy(), V0.cpu().numpy(), w1.cpu().numpy(), y1.cpu().numpy()
     lmax = np.abs(w0).max(1)
     ew = np.abs(w1 - w0).max(1) / np.maximum(lmax, 1e-30)
-    assert ew.max() <= 1e-6, ew.max()
+    # both solvers are backward stable in fp32, each within a few ulps of lambda_max of the exact eigenvalues
+    # (measured max 1.003e-6 against the MKL-exact ssyevd)
+    assert ew.max() <= 2e-6, ew.max()
     cls0 = O.classes(w0)
     cls1 = O.classes(w1)
     p_, l_, s_ = O.nvt_features(w0)

@@ -39,23 +39,59 @@ def test_mean_edge_length_and_d(fan):
     assert abs(l - float(fan["l"])) < 1e-6 * float(fan["l"])
 
 
-def test_nvt1_eigenvalues(fan):
+def test_oracle_eigh_is_mkls_bitwise(golden):
+    """oracle/eigh3_mkl.c (LAPACK ssyevd's loops with MKL 2024.2's AVX-512 fma placement) against torch.linalg.eigh's
+    saved outputs (tests/golden/eigh.npz: random, rank-1 single-voter, NVT-like, PCA covariances down to 1e-6
+    spacing, matrices across ssyevd's and ssteqr's scaling bounds, repeated eigenvalues): every eigenvalue and every
+    eigenvector component bit for bit, so the oracle does not depend on the host's MKL code path."""
+    g = golden("eigh")
+    fams = sorted(k[:-2] for k in g.files if k.endswith("_T"))
+    assert len(fams) >= 14
+    for fam in fams:
+        w, v = O.eigh(g[f"{fam}_T"])
+        np.testing.assert_array_equal(w, g[f"{fam}_w"], err_msg=fam)
+        np.testing.assert_array_equal(v, g[f"{fam}_v"], err_msg=fam)
+
+
+def test_oracle_norm3_is_torchs():
+    """Tensor.norm(dim=1) / F.normalize on CPU float32 accumulate the squares with fmas: norm3 restates it."""
+    import torch
+    rng = np.random.default_rng(3)
+    x = (rng.normal(size=(50_000, 3)) * rng.uniform(1e-3, 1e3, size=(50_000, 1))).astype(np.float32)
+    np.testing.assert_array_equal(O.norm3(x), torch.from_numpy(x).norm(dim=1).numpy())
+
+
+@pytest.mark.parametrize("k", [32, 16])
+def test_nvt1_matches_reference_bitwise(golden, k):
+    """NVT1 of one Processor.denoise loop body (getBetterFilteredNVT + getVUSmoothedNormals, Decompositionor.py:92-106,
+    278-300) on fandisk at k = 32 and at Processor.denoise()'s default k = 16: eigenvalues, eigenvectors and the
+    smoothed normals f_n bit-identical to the reference's run."""
+    fan = golden(f"fandisk_k{k}")
     ci = np.arange(len(fan["pos0"]))
-    w, v = O.better_filtered_nvt(fan["pos0"], fan["n0"], ci, fan["knn32"], math.pi * 5 / 12)
-    np.testing.assert_allclose(w, fan["eigval1"], atol=2e-6)
+    w, v = O.better_filtered_nvt(fan["pos0"], fan["n0"], ci, fan[f"knn{k}"], math.pi * 5 / 12)
+    np.testing.assert_array_equal(w, fan["eigval1"])
+    np.testing.assert_array_equal(v, fan["eigvec1"])
+    np.testing.assert_array_equal(O.vu_smoothed_normals(w, v, fan["n0"]), fan["it1_f_n"])
 
 
-def test_iteration1_stages(fan):
+@pytest.mark.parametrize("k", [32, 16])
+def test_iteration1_stages(golden, k):
+    """One Processor.denoise loop body at k = 32 and at its default k = 16 (Processor.py:119-139): classes, f_n and
+    NVT2's eigenvalues bit-identical to the reference's; positions after each Gauss-Seidel phase within 5e-7 x bbox
+    (the flat step's exp() and global centre are the only operations not restated to the bit: torch's vectorised
+    exp and its float32 mean; measured max 1.8e-7, ~90 % of the rows exact)."""
+    fan = golden(f"fandisk_k{k}")
     knn = O.FrozenKNN(fan["pos0"])
     rec = {}
-    pos, f_n, cls = O.denoise_iteration(fan["pos0"], fan["n0"], knn, float(fan["d"]), 32, 8, record=rec)
-    assert (cls == fan["it1_classes"]).mean() >= 0.999
-    assert np.percentile(angle(f_n, fan["it1_f_n"]), 99.9) < 1e-4
-    np.testing.assert_allclose(rec["eigval2"], fan["it1_eigval2"], atol=2e-6)
+    pos, f_n, cls = O.denoise_iteration(fan["pos0"], fan["n0"], knn, float(fan["d"]), k, 8, record=rec)
+    np.testing.assert_array_equal(cls, fan["it1_classes"])
+    np.testing.assert_array_equal(f_n, fan["it1_f_n"])
+    np.testing.assert_array_equal(rec["eigval2"], fan["it1_eigval2"])
     bbox = np.linalg.norm(fan["pos0"].max(0) - fan["pos0"].min(0))
     for key in range(3):
         dev = np.linalg.norm(rec[f"pos_after_{key}"] - fan[f"it1_pos_after_{key}"], axis=1) / bbox
-        assert np.percentile(dev, 99) < 1e-5, (key, np.percentile(dev, 99))
+        assert (dev == 0).mean() > 0.85 and np.percentile(dev, 99.9) < 1e-7 and dev.max() < 5e-7, \
+            (key, (dev == 0).mean(), np.percentile(dev, 99.9), dev.max())
 
 
 def test_ten_iterations_within_fp32_fp64_envelope(fan):
@@ -93,10 +129,11 @@ def test_nvt_vu_classes(steps, rho, k):
     ci = np.arange(len(pos))
     r = math.pi * 5 / 12 if rho == "a5pi12" else math.pi / 3
     w, v = O.better_filtered_nvt(pos, n1, ci, steps[f"knn{k}"], r)
-    np.testing.assert_allclose(w, steps[f"nvt_{rho}_k{k}_eigval"], atol=2e-6)
-    # smoothing and classification fed the reference's own decomposition
-    vu = O.vu_smoothed_normals(steps[f"nvt_{rho}_k{k}_eigval"], steps[f"nvt_{rho}_k{k}_eigvec"], n1)
-    assert np.percentile(angle(vu, steps[f"nvt_{rho}_k{k}_vu"]), 99.9) < 1e-5
+    # the whole NVT1 chain -- vote, list-order tensor sums, MKL-exact eigh, VU smoothing -- bit for bit
+    np.testing.assert_array_equal(w, steps[f"nvt_{rho}_k{k}_eigval"])
+    np.testing.assert_array_equal(v, steps[f"nvt_{rho}_k{k}_eigvec"])
+    vu = O.vu_smoothed_normals(w, v, n1)
+    np.testing.assert_array_equal(vu, steps[f"nvt_{rho}_k{k}_vu"])
     cls = O.classes(steps[f"nvt_{rho}_k{k}_eigval"])
     assert (cls == steps[f"nvt_{rho}_k{k}_classes"]).all()
     feats = np.stack(O.nvt_features(steps[f"nvt_{rho}_k{k}_eigval"]), 1)
@@ -139,7 +176,7 @@ def test_pca_normals_up_to_sign(steps):
     nbr = O.knn_graph_noself(steps["pos"], 12)
     assert (np.sort(nbr, 1) == np.sort(steps["knn12_noself"], 1)).mean() > 0.999
     n = O.pca_normals_unoriented(steps["pos"], steps["knn12_noself"])
-    assert np.percentile(angle(n, steps["pca_n"]), 99.9) < 1e-3
+    np.testing.assert_array_equal(n, steps["pca_n"])          # torch's reduction order + the MKL-exact eigh
 
 
 def test_lattice_kat(golden):
@@ -199,13 +236,13 @@ def test_martin_feature_decomposition_matches_reference(cpsd):
     pos, n, d = cpsd["pos"], cpsd["n"], float(cpsd["d"])
     slices, j = O.radius_selection(pos, pos, d)
     ci = np.arange(len(pos))
-    w1, _ = O.normal_filtered_nvt(n, ci, slices, j, 0.9)
-    np.testing.assert_allclose(w1, cpsd["nvt_eigval"], atol=2e-6)
+    w1, v1 = O.normal_filtered_nvt(n, ci, slices, j, 0.9)
+    np.testing.assert_array_equal(w1, cpsd["nvt_eigval"])
+    np.testing.assert_array_equal(v1, cpsd["nvt_eigvec"])
     w2, v2, fn = O.martin_feature_decomposition(pos, pos, n, d, 0.9)
-    ang = angle64(fn, cpsd["f_n"])
-    assert ang.max() < 1e-6
-    scale = np.abs(cpsd["pvt_eigval"]).max(1, keepdims=True) + 1e-30
-    assert (np.abs(w2 - cpsd["pvt_eigval"]) / scale).max() < 1e-5
+    np.testing.assert_array_equal(fn, cpsd["f_n"])
+    np.testing.assert_array_equal(w2, cpsd["pvt_eigval"])
+    np.testing.assert_array_equal(v2, cpsd["pvt_eigvec"])
     np.testing.assert_array_equal(O.vu_features(w2, 0.3), cpsd["vu_classes"])
 
 
@@ -227,9 +264,11 @@ def test_cpsd_driver_oracle_matches_reference(golden):
     for it in (1, 2):
         rp, rn = O.cpsd_iteration(pos0, rp, rn, pos0, knn, d)
         dev = np.linalg.norm(rp - c[f"drv_pos_it{it}"], axis=1) / bbox
+        np.testing.assert_array_equal(rn, c[f"drv_n_it{it}"])   # f_n: the radius NVT + VU chain, bit for bit
         if it == 1:
-            assert np.median(dev) < 1e-7 and np.percentile(dev, 99) < 1e-5 and dev.max() < 1e-4, dev.max()
-            assert np.abs(rn - c["drv_n_it1"]).max() < 1e-6
+            # only the flat step's exp() and global centre are not restated to the bit (measured: 99.4 % of the rows
+            # exact, max 5.7e-9 x bbox)
+            assert np.median(dev) == 0 and np.percentile(dev, 99) <= 1e-8 and dev.max() < 1e-7, dev.max()
         else:
             assert np.median(dev) < 1e-5 and np.percentile(dev, 99) < 5e-3, np.percentile(dev, 99)
 
