@@ -553,8 +553,23 @@ def main():
 
     # per-kernel timing (HIP events on the launch stream), outside the timed region
     kernel_ms, knn_ms = {}, float("nan")
+    xchg = None
     if mode == "slab":
         sd.check()      # exactness: no k-ball left its rank's slab + halo
+        if sd.native:
+            # one halo refresh on its own (FIELD_POS: pack -> libpcd comm -> unpack), every rank at once: the median of
+            # 5, max over the ranks (an idempotent refresh between iterations)
+            xs = []
+            for _ in range(5):
+                torch.cuda.synchronize()
+                dist.barrier()
+                tx = time.perf_counter()
+                sd.e.fused.halo_exchange(sd.comm, nat.FIELD_POS)
+                torch.cuda.synchronize()
+                xs.append((time.perf_counter() - tx) * 1e3)
+            xt = torch.tensor([float(np.median(xs))], dtype=torch.float64)
+            dist.all_reduce(xt, op=dist.ReduceOp.MAX)
+            xchg = float(xt)
         ks = [sd.iterate_timed(params) for _ in range(args.profile_steps)]
         if ks:
             kernel_ms = {key: round(float(np.mean([x[key] for x in ks])), 4) for key in ks[0]}
@@ -685,9 +700,17 @@ def main():
         counts = torch.tensor([sd.owned_global.numel(), sd.halo_points], dtype=torch.int64)
         allc = [torch.zeros_like(counts) for _ in range(world)]
         dist.all_gather(allc, counts)
+        # halo traffic: every received halo row is refreshed once per exchange -- f_n after K1, then the positions
+        # after each Gauss-Seidel phase (once per iteration in the Jacobi mode) -- as 12-byte rows on the RCCL path
+        n_x = 1 + (1 if params.jacobi else params.nphases)
+        xb = [int(c[1]) * 12 * n_x for c in allc]
         out["slab"] = {"world": info["world"], "transport": info["transport"],
                        "owned_rows": [int(c[0]) for c in allc], "halo_rows": [int(c[1]) for c in allc],
-                       "halo": sd.halo, "replans": sd.replans, "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
+                       "halo": sd.halo, "replans": sd.replans, "replan_log": sd.replan_log,
+                       "exchanges_per_iteration": n_x, "exchange_bytes_per_iteration": sum(xb),
+                       "exchange_bytes_per_iteration_max_rank": max(xb),
+                       "exchange_ms": None if xchg is None else round(xchg, 4),
+                       "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
                        "note": ("every rank on GPU 0 over libpcd's host transport: a rehearsal, not a scaling number"
                                 if args.rehearse_one_gpu else
                                 "one GPU per rank, halo rows and the flat phase's scalars over libpcd's RCCL "

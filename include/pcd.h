@@ -237,9 +237,15 @@ int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n
 /* Device error word -> status: PCD_ERR_STATE if a kNN list held an invalid entry or (spatial slabs) a query's
  * k-ball left the coverage box.  Synchronises `stream`.  store() calls it. */
 int pcd_denoiser_check(pcd_denoiser* dn, void* stream);
-/* The raw device error word behind check (bit 0: invalid list entry, bit 1: a k-ball left the coverage box), without
- * raising: the spatial-slab driver widens its halo and re-plans on bit 1.  Synchronises `stream`. */
+/* The raw device error word behind check (bit 0: invalid list entry, bit 1: a k-ball left the coverage box; with bit
+ * 1, bit 2: a row without a coverage sphere failed -- the band -- and bit 3: a sphere row failed), without raising:
+ * the spatial-slab driver re-plans on bit 1.  Synchronises `stream`. */
 int pcd_denoiser_status(pcd_denoiser* dn, int* bits, void* stream);
+/* What the failed coverage checks lacked, for a re-plan that grows only that (spatial slabs; no reference
+ * counterpart): band_excess = the farthest any sphere-less row's k-ball reached past the coverage box
+ * (0: none failed), sphere_ratio = the largest (|q - centre| + d_k) / R over the sphere rows that failed (0: none).
+ * Synchronises `stream`. */
+int pcd_denoiser_coverage_excess(pcd_denoiser* dn, float* band_excess, float* sphere_ratio, void* stream);
 /* The kNN list the last K1 stage stored (the snapshot's `cols` nearest of each point's current position, in
  * (distance, index) order = getKNNSelection's columns, Selector.py:235-246), in caller order with ORIGINAL snapshot
  * indices: out int64 [N][cols], cols <= the stored list length (max(k, k_update) of the last iteration). */

@@ -20,8 +20,6 @@
 #include <cstring>
 #include <vector>
 
-#include <rocprim/rocprim.hpp>
-
 #include "pcd_knn.h"
 #include "pcd_lists.h"
 #include "pcd_ops.h"
@@ -183,6 +181,25 @@ struct Cover {
         const float m = sqrtf(sq3(q - v3(o.x, o.y, o.z))) * 1.000001f + sqrtf(d2) * 1.000001f + 1e-30f;
         return m <= R * (1.f - 1e-6f);
     }
+    // the coverage check of row i: on a failure, err[0] |= 2 and what failed -- bit 4: a row without a sphere (the
+    // band; err[1] = atomic max of how far its ball reaches past the box, float bits), bit 8: a sphere row (err[2] =
+    // atomic max of (|q - centre| + d_k) / R) -- so a re-plan grows only what failed, by what it lacked
+    PCD_DEV void check_row(int* err, int64_t i, Vec3 q, float d2) const {
+        if (holds_row(i, q, d2)) return;
+        const float r = sqrtf(d2) * 1.000001f + 1e-30f;
+        const float R = xr ? xr[i] : 0.f;
+        if (R > 0.f) {
+            const float4 o = org[i];
+            const float m = sqrtf(sq3(q - v3(o.x, o.y, o.z))) * 1.000001f + r;
+            atomicOr(err, 2 | 8);
+            atomicMax(err + 2, __float_as_int(m / R));
+        } else {
+            const float ex = fmaxf(fmaxf(fmaxf(lo[0] - (q.x - r), (q.x + r) - hi[0]), fmaxf(lo[1] - (q.y - r), (q.y + r) - hi[1])),
+                                   fmaxf(lo[2] - (q.z - r), (q.z + r) - hi[2]));
+            atomicOr(err, 2 | 4);
+            atomicMax(err + 1, __float_as_int(fmaxf(ex, 0.f)));   // (non-negative floats order as their bits)
+        }
+    }
 };
 
 // Spatial slabs: the rank's OWN slab (the points it owns, no halo).  K1 marks every active row whose k-ball is not
@@ -216,19 +233,14 @@ PCD_DEV void k1_epilogue(const float4* __restrict__ pos, const float4* __restric
     }
     store_list<K, true>(idx, N, i, kstore, l);   // streamed: keep L2 for the gathers
     if (bad) atomicOr(err, 1);
-    if (!cov.holds_row(i, vi, dk)) atomicOr(err, 2);
+    cov.check_row(err, i, vi, dk);
     band.mark(t0, vi, dk);
-#ifdef PCD_EXP_NONVT
-    const float4 n4 = nrm[i];
-    __builtin_nontemporal_store(v4f{n4.x, n4.y, n4.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
-#else
     const Sym3 T = nvt_tensor<K>(Rows4{pos}, Rows4{nrm}, vi, k, RegNb32{l}, rho, BlkNbSafe{idx, N, i});
     const float4 n4 = nrm[i];
     float w[3], V[3][3];
     eigh3(T, w, V);
     const Vec3 f = vu_smooth(w, V, v3(n4.x, n4.y, n4.z), tau, damp);
     __builtin_nontemporal_store(v4f{f.x, f.y, f.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
-#endif
 }
 
 // K1: kNN + NVT1 + VU smoothing.
@@ -311,9 +323,6 @@ PCD_DEV bool anchor_holds(float d2k, Vec3 q, float4 a) {
 // (an exact d² tie included, which the rank would break) sends the row to the redo search instead.  The
 // certificate counts candidates below the squared anchor bound, a rounding-safe restatement of anchor_holds.
 // Rows that fail take the exact redo path, so the stored lists are bit-identical to the 64-bit-key ordering.
-#ifndef PCD_ANCHOR_SORT
-#define PCD_ANCHOR_SORT oddeven_sort
-#endif
 #ifndef PCD_ANCHOR_BS
 #define PCD_ANCHOR_BS 128
 #endif
@@ -321,43 +330,22 @@ static constexpr int kAnchorBS = PCD_ANCHOR_BS;
 #ifndef PCD_ANCHOR_OCC
 #define PCD_ANCHOR_OCC 1
 #endif
-// The slot -> rank map in LDS as 24-bit offsets from the set's first (smallest) rank: 192 B a lane instead of 256,
-// room for 3 waves per SIMD instead of 2 (a set whose ranks span 2^24 or more -- only past 16M points, at the top
-// Morton boundaries -- fails the test and is re-anchored exactly).
-#ifndef PCD_ANCHOR_MAP24
-#define PCD_ANCHOR_MAP24 0
-#endif
-#ifndef PCD_ANCHOR_SPLIT
-#define PCD_ANCHOR_SPLIT 1   // 0: one 64-key network; 2: four quarters (A/B at 10M: anchor test 1.29 / 1.26 / 1.31 ms at 0 / 1 / 2)
-#endif
-#ifndef PCD_DENSE_PRE
-#define PCD_DENSE_PRE 2      // the dense radii (1) and query boxes (2) by a lane-per-row pass before the dense anchoring (k_dense_radius): first iteration 21.1 -> 19.6 -> 19.1 ms (A/B at 10M)
-#endif
-#ifndef PCD_ANCHOR_PRELOAD
-#define PCD_ANCHOR_PRELOAD 1  // the whole anchor set's blocks loaded with the row's own loads (two-halves variant): anchor test 1.306 -> 1.29 ms, 211 -> 181 VGPRs
-#endif
-#ifndef PCD_ANCHOR_BATCH
-#define PCD_ANCHOR_BATCH 64   // anchor-set slots gathered per batch (all of them by default)
-#endif
+// (measured and dropped, DESIGN.md §3 tried table: a 24-bit LDS slot map at 3 waves/SIMD, four 16-slot quarters,
+// smaller gather batches, anchor sets reloaded after the first half's sort)
 template <int K, int KA>
 __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridView g, const float4* __restrict__ pos, int64_t N,
                                                           RowMap rm, int kstore, const float4* __restrict__ anc,
-                                                          const int32_t* __restrict__ alist,
+                                                          const float* __restrict__ ak1, const int32_t* __restrict__ alist,
                                                           int32_t* __restrict__ idx, uint8_t* __restrict__ fail) {
     static_assert(KA == 2 * K && KA <= 64, "anchor lists hold twice the list cap; 6 slot bits");
-#if PCD_ANCHOR_MAP24
-    __shared__ uint16_t s_lo[KA * kAnchorBS];
-    __shared__ uint8_t s_hi[KA * kAnchorBS];
-#else
     __shared__ uint32_t s_r[KA * kAnchorBS];
-#endif
     const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * kAnchorBS + threadIdx.x;
     bool failed = false;
     if (t0 < rm.nq) {
         const int64_t i = rm(t0);
-#if PCD_ANCHOR_PRELOAD
         // every block of the anchor set issued with the row's own loads (they depend on the row only): the second
         // half's ranks are not fetched after the first half's keys, one HBM round trip off the critical path
+        // (anchor test 1.306 -> 1.29 ms, 211 -> 181 VGPRs)
         v4i pre[KA / 4];
 #pragma unroll
         for (int g8 = 0; g8 < KA / 8; ++g8) {
@@ -365,7 +353,6 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
             pre[2 * g8] = __builtin_nontemporal_load(lp);
             pre[2 * g8 + 1] = __builtin_nontemporal_load(lp + 1);
         }
-#endif
         const float4 p4 = pos[i];
         const Vec3 vi = v3(p4.x, p4.y, p4.z);
         const float4 a = anc[i];
@@ -380,114 +367,35 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
             // every list point is within D of the anchor, hence within D + delta of q
             const float R = (a.w + delta) * (1.f + 1e-5f);
             const float S = 67108864.f / fmaxf(R * R, 1e-30f);
+            // the members that can rank among the first kstore + 1 at q: distance band <= cut (pcd_lists.h); the
+            // others read the +inf sentinel row instead (one line every such lane of the wave shares: an infinite
+            // key, they sort last, below stays exact for the certificate)
+            const uint32_t cut = anchor_cut(ak1[i], delta * (1.f + kAnchorEps), a.w);
             uint32_t c[KA];
             int below = 0;
-#if PCD_ANCHOR_MAP24
-            uint32_t base = 0;
-            bool span_ok = true;
-#endif
             // slot t -> snapshot rank rt into the LDS map
-            auto map_store = [&](int t, uint32_t rt) {
-#if PCD_ANCHOR_MAP24
-                const uint32_t dl = rt - base;
-                span_ok = span_ok && dl < (1u << 24);
-                s_lo[t * kAnchorBS + threadIdx.x] = (uint16_t)dl;
-                s_hi[t * kAnchorBS + threadIdx.x] = (uint8_t)(dl >> 16);
-#else
-                s_r[t * kAnchorBS + threadIdx.x] = rt;
-#endif
-            };
-            if constexpr (PCD_ANCHOR_SPLIT == 2 && KA == 64) {
-            // four quarters of 16 slots, each quarter's gathers in flight while the previous quarter's keys sort; the
-            // sorted quarters merge pairwise (bitonic, 32 each), then as in the two-halves variant
-            uint32_t qa[16], qb[16], qc[16], qd[16], ma[32], mb[32];
-            auto quarter = [&](int h, uint32_t (&cc)[16], auto&& between) {
-                uint32_t r[16];
-#pragma unroll
-                for (int g8 = 0; g8 < 2; ++g8) {
-                    const v4i* lp = lblock(alist, N, i, 2 * h + g8);
-                    const v4i x = __builtin_nontemporal_load(lp), y = __builtin_nontemporal_load(lp + 1);
-                    r[8 * g8 + 0] = (uint32_t)x.x; r[8 * g8 + 1] = (uint32_t)x.y; r[8 * g8 + 2] = (uint32_t)x.z;
-                    r[8 * g8 + 3] = (uint32_t)x.w; r[8 * g8 + 4] = (uint32_t)y.x; r[8 * g8 + 5] = (uint32_t)y.y;
-                    r[8 * g8 + 6] = (uint32_t)y.z; r[8 * g8 + 7] = (uint32_t)y.w;
-                }
-#if PCD_ANCHOR_MAP24
-                if (h == 0) base = min(r[0], (uint32_t)N);    // (the set is stored in rank order: its smallest rank)
-#endif
-                float4 pj[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    const uint32_t rt = min(r[u], (uint32_t)N);
-                    map_store(16 * h + u, rt);
-                    pj[u] = *at32(g.pts, rt);
-                }
-                between();
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    const float d2 = dist2(vi, pj[u]);
-                    below += d2 < T ? 1 : 0;
-                    cc[u] = ((uint32_t)fminf(d2 * S, 67108860.f) << 6) | (uint32_t)(16 * h + u);
-                }
-            };
-            // two sorted 16-runs -> one sorted 32-run: the second reversed makes the pair bitonic
-            auto merge16 = [](const uint32_t (&x)[16], const uint32_t (&y)[16], uint32_t (&z)[32]) {
-#pragma unroll
-                for (int u = 0; u < 16; ++u) { z[u] = x[u]; z[16 + u] = y[15 - u]; }
-#pragma unroll
-                for (int d = 16; d > 0; d >>= 1)
-#pragma unroll
-                    for (int u = 0; u < 32; ++u)
-                        if ((u & d) == 0) cswap(z[u], z[u + d]);
-            };
-            quarter(0, qa, [] {});
-            quarter(1, qb, [&] { oddeven_sort<16>(qa); });
-            quarter(2, qc, [&] { oddeven_sort<16>(qb); merge16(qa, qb, ma); });
-            quarter(3, qd, [&] { oddeven_sort<16>(qc); });
-            oddeven_sort<16>(qd);
-            merge16(qc, qd, mb);
-            uint32_t c33 = 0xFFFFFFFFu;
-#pragma unroll
-            for (int u = 0; u < 32; ++u) {
-                const uint32_t lo = min(ma[u], mb[31 - u]), hi = max(ma[u], mb[31 - u]);
-                ma[u] = lo;
-                c33 = min(c33, hi);
-            }
-#pragma unroll
-            for (int d = 16; d > 0; d >>= 1)
-#pragma unroll
-                for (int u = 0; u < 32; ++u)
-                    if ((u & d) == 0) cswap(ma[u], ma[u + d]);
-#pragma unroll
-            for (int u = 0; u < 32; ++u) c[u] = ma[u];
-            c[32] = c33;
-            } else if constexpr (PCD_ANCHOR_SPLIT == 1 && KA == 64) {
+            auto map_store = [&](int t, uint32_t rt) { s_r[t * kAnchorBS + threadIdx.x] = rt; };
+            if constexpr (KA == 64) {
             // two halves of 32 slots: the second half's gathers are in flight while the first half's keys sort; the
             // sorted halves merge by a half-cleaner (its low side: the 32 smallest, bitonic; its high side's minimum:
             // the 33rd) and a 32-wide bitonic merge -- the same first kstore + 1 keys as the 64-key network
+            // (anchor test 1.29 -> 1.26 ms)
             uint32_t ca[32], cb[32];
             auto half = [&](int h, uint32_t (&cc)[32], auto&& between) {
                 uint32_t r[32];
 #pragma unroll
                 for (int g8 = 0; g8 < 4; ++g8) {
-#if PCD_ANCHOR_PRELOAD
                     const v4i x = pre[2 * (4 * h + g8)], y = pre[2 * (4 * h + g8) + 1];
-#else
-                    const v4i* lp = lblock(alist, N, i, 4 * h + g8);
-                    const v4i x = __builtin_nontemporal_load(lp), y = __builtin_nontemporal_load(lp + 1);
-#endif
                     r[8 * g8 + 0] = (uint32_t)x.x; r[8 * g8 + 1] = (uint32_t)x.y; r[8 * g8 + 2] = (uint32_t)x.z;
                     r[8 * g8 + 3] = (uint32_t)x.w; r[8 * g8 + 4] = (uint32_t)y.x; r[8 * g8 + 5] = (uint32_t)y.y;
                     r[8 * g8 + 6] = (uint32_t)y.z; r[8 * g8 + 7] = (uint32_t)y.w;
                 }
-#if PCD_ANCHOR_MAP24
-                if (h == 0) base = min(r[0], (uint32_t)N);    // (the set is stored in rank order: its smallest rank)
-#endif
                 float4 pj[32];
 #pragma unroll
                 for (int u = 0; u < 32; ++u) {
-                    const uint32_t rt = min(r[u], (uint32_t)N);
+                    const uint32_t rt = min(anchor_rank(r[u]), (uint32_t)N);
                     map_store(32 * h + u, rt);
-                    pj[u] = *at32(g.pts, rt);
+                    pj[u] = *at32(g.pts, anchor_band(r[u]) <= cut ? rt : (uint32_t)N);
                 }
                 between();
 #pragma unroll
@@ -516,45 +424,32 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
             for (int u = 0; u < 32; ++u) c[u] = ca[u];
             c[32] = c33;
             } else {
-            // the set's ranks and rows in batches of AB slots (AB = KA: every gather in flight at once; a smaller batch
-            // holds fewer rows in registers, a scheduling barrier keeping the next batch's loads behind this one's keys)
-            constexpr int AB = PCD_ANCHOR_BATCH < KA ? PCD_ANCHOR_BATCH : KA;
-            static_assert(KA % AB == 0 && AB % 8 == 0, "whole 8-column blocks per batch");
+            // K <= 16: every gather of the set in flight at once, then one KA-key network
+            uint32_t r[KA];
 #pragma unroll
-            for (int b0 = 0; b0 < KA; b0 += AB) {
-                uint32_t r[AB];
-#pragma unroll
-                for (int g8 = 0; g8 < AB / 8; ++g8) {
-                    const v4i* lp = lblock(alist, N, i, b0 / 8 + g8);
-                    const v4i x = __builtin_nontemporal_load(lp), y = __builtin_nontemporal_load(lp + 1);
-                    r[8 * g8 + 0] = (uint32_t)x.x; r[8 * g8 + 1] = (uint32_t)x.y; r[8 * g8 + 2] = (uint32_t)x.z;
-                    r[8 * g8 + 3] = (uint32_t)x.w; r[8 * g8 + 4] = (uint32_t)y.x; r[8 * g8 + 5] = (uint32_t)y.y;
-                    r[8 * g8 + 6] = (uint32_t)y.z; r[8 * g8 + 7] = (uint32_t)y.w;
-                }
-#if PCD_ANCHOR_MAP24
-                if (b0 == 0) base = min(r[0], (uint32_t)N);   // (the set is stored in rank order: its smallest rank)
-#endif
-#pragma unroll
-                for (int u = 0; u < AB; ++u) {
-                    const int t = b0 + u;
-                    // an unused slot of a partial anchor set holds N: the snapshot's +inf sentinel row (the min keeps
-                    // any entry inside the allocation)
-                    const uint32_t rt = min(r[u], (uint32_t)N);
-                    map_store(t, rt);
-                    const float d2 = dist2(vi, *at32(g.pts, rt));   // unconditional load: the batch's gathers in flight
-                    below += d2 < T ? 1 : 0;
-                    // clamp below 2^26 in fp32 (2^26 - 1 rounds UP to 2^26, which would wrap to 0 after the shift);
-                    // only the sentinel's infinite distance reaches it
-                    c[t] = ((uint32_t)fminf(d2 * S, 67108860.f) << 6) | (uint32_t)t;
-                }
-                if (AB < KA) __builtin_amdgcn_sched_barrier(0);
+            for (int g8 = 0; g8 < KA / 8; ++g8) {
+                const v4i* lp = lblock(alist, N, i, g8);
+                const v4i x = __builtin_nontemporal_load(lp), y = __builtin_nontemporal_load(lp + 1);
+                r[8 * g8 + 0] = (uint32_t)x.x; r[8 * g8 + 1] = (uint32_t)x.y; r[8 * g8 + 2] = (uint32_t)x.z;
+                r[8 * g8 + 3] = (uint32_t)x.w; r[8 * g8 + 4] = (uint32_t)y.x; r[8 * g8 + 5] = (uint32_t)y.y;
+                r[8 * g8 + 6] = (uint32_t)y.z; r[8 * g8 + 7] = (uint32_t)y.w;
             }
-            PCD_ANCHOR_SORT<KA>(c);
+#pragma unroll
+            for (int t = 0; t < KA; ++t) {
+                // an unused slot of a partial anchor set holds N: the snapshot's +inf sentinel row (the min keeps
+                // any entry inside the allocation)
+                const uint32_t rt = min(anchor_rank(r[t]), (uint32_t)N);
+                map_store(t, rt);
+                // unconditional load: every gather in flight (members past the cut read the sentinel row)
+                const float d2 = dist2(vi, *at32(g.pts, anchor_band(r[t]) <= cut ? rt : (uint32_t)N));
+                below += d2 < T ? 1 : 0;
+                // clamp below 2^26 in fp32 (2^26 - 1 rounds UP to 2^26, which would wrap to 0 after the shift);
+                // only the sentinel's infinite distance reaches it
+                c[t] = ((uint32_t)fminf(d2 * S, 67108860.f) << 6) | (uint32_t)t;
+            }
+            oddeven_sort<KA>(c);
             }
             bool ok = below >= kstore;
-#if PCD_ANCHOR_MAP24
-            ok = ok && span_ok;
-#endif
 #pragma unroll
             for (int t = 0; t < K; ++t)
                 if (t < kstore) ok = ok && (c[t] >> 6) < (c[t + 1] >> 6);
@@ -562,14 +457,7 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
             if (ok) {
                 int out[K];
 #pragma unroll
-                for (int t = 0; t < K; ++t) {
-#if PCD_ANCHOR_MAP24
-                    const uint32_t sl = (c[t] & 63u) * kAnchorBS + threadIdx.x;
-                    out[t] = (int32_t)(base + (((uint32_t)s_hi[sl] << 16) | (uint32_t)s_lo[sl]));
-#else
-                    out[t] = (int32_t)s_r[(c[t] & 63u) * kAnchorBS + threadIdx.x];
-#endif
-                }
+                for (int t = 0; t < K; ++t) out[t] = (int32_t)s_r[(c[t] & 63u) * kAnchorBS + threadIdx.x];
                 store_list<K, true>(idx, N, i, kstore, out);
             }
         }
@@ -640,7 +528,7 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
 #pragma unroll
         for (int t = 0; t < K; ++t)
             if (t == kstore - 1) dk = dist2(vi, g.pts[l[t]]);
-        if (!cov.holds_row(i, vi, dk)) atomicOr(err, 2);
+        cov.check_row(err, i, vi, dk);
         band.mark(t0, vi, dk);
     }
     // 4 neighbours in flight per batch (8 measured 0.06 ms slower at 10M: the VGPRs of 8 rows in flight)
@@ -652,13 +540,9 @@ __device__ __forceinline__ void nvt1_row(const GridView& g, const float4* __rest
     __builtin_nontemporal_store(v4f{f.x, f.y, f.z, 0.f}, reinterpret_cast<v4f*>(fn + i));
 }
 
-// Every active row, or (skip != null) every active row t with skip[t] == 0: the rows the anchor test certified,
-// run on a side stream while the re-anchoring search works on the others (pcd_denoiser::side).
+// Every active row, its neighbours read through the block's LDS row window (without it: 1.38 ms instead of 1.01).
 // UNIT: the normals are the loop's own normalised f_n (every iteration after the first since load): the vote's
 // margin is a constant (nvt_tensor).
-#ifndef PCD_NVT1_WIN
-#define PCD_NVT1_WIN 1
-#endif
 #ifndef PCD_NVT1_OCC
 #define PCD_NVT1_OCC 1
 #endif
@@ -666,38 +550,14 @@ template <int K, bool UNIT>
 __global__ __launch_bounds__(kNvtBS, PCD_NVT1_OCC) void k_nvt1(GridView g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                int kstore, float rho, float tau, float damp, Cover cov,
-                                               float4* __restrict__ fn, int* __restrict__ err, int win,
-                                               const uint8_t* __restrict__ skip, Band band) {
-#if PCD_NVT1_WIN
+                                               float4* __restrict__ fn, int* __restrict__ err, int win, Band band) {
     __shared__ float4 s_pos[kWinRows], s_nrm[kWinRows];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
     const int64_t lo = stage_window(pos, nrm, N, rm(b0), s_pos, s_nrm, win);
     const int64_t t0 = b0 + threadIdx.x;
     if (t0 >= rm.nq) return;
-    if (skip && skip[t0]) return;
     nvt1_row<K, UNIT>(g, pos, nrm, idx, N, rm(t0), k, kstore, rho, tau, damp, cov, fn, err, WinRows<>{pos, s_pos, lo},
                 WinRows<>{nrm, s_nrm, lo}, band, t0);
-#else
-    (void)win;
-    const int64_t t0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    if (t0 >= rm.nq) return;
-    if (skip && skip[t0]) return;
-    nvt1_row<K, UNIT>(g, pos, nrm, idx, N, rm(t0), k, kstore, rho, tau, damp, cov, fn, err, Rows4{pos}, Rows4{nrm},
-                      band, t0);
-#endif
-}
-
-// The rows of list[0 .. *cnt) (the re-anchored rows, spatially sparse: no LDS window), grid-stride.
-template <int K>
-__global__ __launch_bounds__(256) void k_nvt1_list(GridView g, const float4* __restrict__ pos,
-                                                    const float4* __restrict__ nrm, const int32_t* __restrict__ idx,
-                                                    int64_t N, int k, int kstore, float rho, float tau, float damp,
-                                                    Cover cov, float4* __restrict__ fn, int* __restrict__ err,
-                                                    const int32_t* __restrict__ list, const unsigned* __restrict__ cnt) {
-    const int64_t n = (int64_t)*cnt;
-    for (int64_t t = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x; t < n;
-         t += (int64_t)gridDim.x * blockDim.x)
-        nvt1_row<K, false>(g, pos, nrm, idx, N, list[t], k, kstore, rho, tau, damp, cov, fn, err, Rows4{pos}, Rows4{nrm});
 }
 
 // Re-anchor: the exact KA nearest at the current position, one query per WAVE (pcd_wknn.h), capped by the old
@@ -712,7 +572,7 @@ __global__ __launch_bounds__(256) void k_nvt1_list(GridView g, const float4* __r
 #endif
 template <int KA, bool DENSE>
 __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g, const float4* __restrict__ pos, int64_t N, RowMap rm,
-                                                        int kstore, float4* __restrict__ anc,
+                                                        int kstore, float4* __restrict__ anc, float* __restrict__ ak1,
                                                         int32_t* __restrict__ alist, int32_t* __restrict__ idx,
                                                         const int32_t* __restrict__ redo,
                                                         const unsigned* __restrict__ redo_cnt, int* __restrict__ err) {
@@ -731,7 +591,7 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
             const float4 a = anc[i];
             // (D + |q - a|)² bounds the KA-th key at q only for a FULL anchor set (KA points within D of a); a partial
             // set (fewer points within its radius, unused slots = N, the +inf sentinel row) gives no such bound
-            if (a.w >= 0.f && (uint32_t)alist[lpos(N, i, KA - 1)] < (uint32_t)N) cap = anchor_cap(q, a);
+            if (a.w >= 0.f && anchor_rank((uint32_t)alist[lpos(N, i, KA - 1)]) < (uint32_t)N) cap = anchor_cap(q, a);
         }
         const unsigned long long top = wave_knn<KA>(g, q, cap, s_buf[wv], &s_cells[wv], lane);
         // a slot without a finite candidate (non-finite query, fewer than KA points) is never stored as an index:
@@ -742,21 +602,24 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
         const bool all_valid = !__any(lane < KA && !valid);
         if (!all_valid && lane == 0) atomicOr(err, 1);
         if (lane < kstore) idx[lpos(N, i, lane)] = r;   // (whole 32-B sectors, pcd_lists.h)
+        // D: the KA-th distance (every other snapshot point is at least this far from the anchor); ak1: the
+        // (K+1)-th, rounded up (the anchor test's gather cut, pcd_lists.h anchor_entry)
+        const float D = sqrtf(__uint_as_float((unsigned)__shfl((int)(unsigned)(top >> 32), KA - 1)));
+        const float dK = sqrtf(__uint_as_float((unsigned)__shfl((int)(unsigned)(top >> 32), KA / 2)));
         {   // the anchor set in rank order (see k_knn_requery), unused slots last
-            uint32_t v[1] = {lane < KA ? (uint32_t)r : 0xFFFFFFFFu};
+            uint32_t v[1] = {lane < KA ? anchor_entry((uint32_t)r, sqrtf(__uint_as_float((unsigned)(top >> 32))), D)
+                                       : 0xFFFFFFFFu};
             grp_bitonic_sort32<64, 1>(v, lane);
             if (lane < KA) alist[lpos(N, i, lane)] = (int32_t)v[0];
         }
-        // D: the KA-th distance (every other snapshot point is at least this far from the anchor)
-        if (lane == KA - 1)
-            anc[i] = make_float4(q.x, q.y, q.z, all_valid ? sqrtf(__uint_as_float((unsigned)(top >> 32))) : __int_as_float(0x7FC00000));
+        if (lane == 0) {
+            anc[i] = make_float4(q.x, q.y, q.z, all_valid ? D : __int_as_float(0x7FC00000));
+            ak1[i] = dK * (1.f + 1e-5f);
+        }
     }
 }
 
 // K2: NVT2 on f_n -> classes + edge vectors.
-#ifndef PCD_NVT2_NORM
-#define PCD_NVT2_NORM false
-#endif
 #ifndef PCD_NVT2_OCC
 #define PCD_NVT2_OCC 1
 #endif
@@ -780,24 +643,18 @@ __global__ __launch_bounds__(kNvtBS, PCD_NVT2_OCC) void k_nvt2(const float4* __r
     int wsum = 0;
     int l[K];
     load_list<K, true>(idx, N, i, k, l);   // read once: streamed past L2 so the neighbour gathers keep it
-    const Sym3 T = nvt_tensor<K, PCD_NVT2_NORM, true>(WinRows<kWinHaloNvt2, kNvtBS>{pos, s_pos, lo}, WinRows<kWinHaloNvt2, kNvtBS>{fn, s_fn, lo},
+    const Sym3 T = nvt_tensor<K, false, true>(WinRows<kWinHaloNvt2, kNvtBS>{pos, s_pos, lo}, WinRows<kWinHaloNvt2, kNvtBS>{fn, s_fn, lo},
                                                 v3(p4.x, p4.y, p4.z), k, RegNb32{l}, rho, BlkNbSafe{idx, N, i},
                                                 &wsum);   // (unconditional: a selected pointer would keep wsum in scratch)
-#ifdef PCD_NVT2_LAPACK
-    float w[3], V[3][3];
-    eigh3(T, w, V);
-    const Vec3 y = v3(V[0][0], V[1][0], V[2][0]);
-#else
     float w[3];
     Vec3 y;
     eigh3_min(T, w, y);
-#endif
     cls[i] = (uint8_t)classify(w, scale, nullptr);
     store4(edge, i, y);
     // parity probe (pcd_denoiser_set_probe): the eigenvalues of the reference's normalised tensor T / Σw
     // (Decompositionor.py:299-300) as this kernel computes them, and Σw
     if (probe) {
-        const float c = PCD_NVT2_NORM ? 1.f : (float)wsum;
+        const float c = (float)wsum;
         probe[i] = make_float4(w[0] / c, w[1] / c, w[2] / c, (float)wsum);
     }
 }
@@ -989,9 +846,6 @@ __global__ void k_copy_delta(const float* __restrict__ from, float* __restrict__
 }
 
 // K3: one Gauss-Seidel phase: active points of class c move (reading pin), other active points copy through.
-#ifndef PCD_PHASE_WIN
-#define PCD_PHASE_WIN 1
-#endif
 // SPLIT (the fused loop's three Gauss-Seidel phases over every row, one class each): no phase copies the rows it
 // does not move.  Every phase reads pin and writes its own class's rows to pout, so after phase ph a row's current
 // position is in pout if its class was moved by an earlier phase (bit cls of `moved`) and in pin otherwise; after the
@@ -1020,7 +874,7 @@ __global__ __launch_bounds__(256, PCD_PHASE_OCC) void k_phase(const float4* __re
                                                 const float4* __restrict__ orig, float clampg, uint32_t moved,
                                                 RowSel sel) {
     // the flat phase moves most rows: its neighbour rows come from an LDS window of pin / fn around the block
-    constexpr bool WIN = PCD_PHASE_WIN && (KIND == PCD_STEP_FLAT);
+    constexpr bool WIN = KIND == PCD_STEP_FLAT;
     __shared__ float4 s_pos[WIN ? WinSize<kWinHaloPhase, 256>::rows : 1], s_fn[WIN ? WinSize<kWinHaloPhase, 256>::rows : 1];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
     const int64_t t0 = b0 + threadIdx.x;
@@ -1132,16 +986,13 @@ struct pcd_denoiser {
     bool seeding = true;          // use the stored list as an acceptance cap (pcd_denoiser_set_seeding)
     // anchored kNN (list cap <= 32): anchors + their 2K-lists, the redo list of queries that failed the test
     float4* anc = nullptr;
+    float* ak1 = nullptr;         // per row: the anchor set's (K+1)-th distance, rounded up (the anchor test's gather cut)
     int32_t* alist = nullptr;
     int32_t* redo = nullptr;      // rows that failed the anchor test (redo list)
     int32_t* spill = nullptr;     // rows the re-anchoring search hands to the exact-key wave search
     RqStats* rqs = nullptr;       // lengths of the redo and spill lists (pcd_qknn.h)
     uint8_t* fail = nullptr;      // per active row: anchor test failed
-    void* sel_tmp = nullptr;      // rocprim::select scratch
-    size_t sel_bytes = 0;
     int anchor_ka = 0;            // KA of the stored anchors (0: none)
-    hipStream_t side = nullptr;   // NVT1 of the certified rows, concurrent with the re-anchoring search
-    hipEvent_t fork = nullptr, join = nullptr;
     int64_t last_dense = -1;      // rows of the last anchored stage when it re-anchored every row, else -1
     bool anchoring = true;        // anchored kNN for seeded searches (pcd_denoiser_set_anchoring)
     bool unit_nrm = false;        // nrm holds the loop's own normalised f_n (set by finish, cleared by load / writes)
@@ -1183,12 +1034,6 @@ static void destroy_cpsd_state(pcd_denoiser* dn);       // (pcd_cpsd.h)
 #ifndef PCD_NUM_PART
 #define PCD_NUM_PART 2048
 #endif
-#ifndef PCD_PHASE_SPLIT
-#define PCD_PHASE_SPLIT 1     // copy-free Gauss-Seidel phases in pcd_denoiser_iterate (k_phase SplitRows)
-#endif
-#ifndef PCD_MAXDIST_PRUNE
-#define PCD_MAXDIST_PRUNE 1   // the max-distance pass skips the blocks whose row box cannot hold the maximum
-#endif
 static const int kNumPart = PCD_NUM_PART;   // blocks of the flat reductions (grid-stride), = their partials
 // Timing events per iteration: start, after the anchor test (+ redo-list select), after the re-anchoring search,
 // after the exact-key spill search, after NVT1 (= end of K1), after NVT2, after each of 3 phases, after finish, end.
@@ -1219,46 +1064,14 @@ static bool phase_is_global(const pcd_denoise_params* p, int ph) {
     return p->phase_kind[ph] == PCD_STEP_FLAT || p->phase_kind[ph] == PCD_STEP_NEW;
 }
 
-// rows whose anchor test failed (fail[t] != 0), in row order -> list[0 .. *cnt)
-static int select_rows(pcd_denoiser* dn, const RowMap& rm, int32_t* list, unsigned* cnt, hipStream_t st) {
-    const size_t n = (size_t)rm.nq;
-    size_t bytes = 0;
-    rocprim::counting_iterator<int32_t> ids(0);
-    if (rm.rows) (void)rocprim::select(nullptr, bytes, rm.rows, dn->fail, list, cnt, n, st);
-    else (void)rocprim::select(nullptr, bytes, ids, dn->fail, list, cnt, n, st);
-    if (bytes > dn->sel_bytes) {
-        (void)hipFree(dn->sel_tmp);
-        dn->sel_tmp = nullptr;
-        dn->sel_bytes = 0;
-        if (hipMalloc(&dn->sel_tmp, bytes) != hipSuccess) return fail(PCD_ERR_OOM, "pcd_denoiser: select temp");
-        dn->sel_bytes = bytes;
-    }
-    hipError_t e = rm.rows ? rocprim::select(dn->sel_tmp, bytes, rm.rows, dn->fail, list, cnt, n, st)
-                           : rocprim::select(dn->sel_tmp, bytes, ids, dn->fail, list, cnt, n, st);
-    if (e != hipSuccess) return fail(PCD_ERR_HIP, std::string("rocprim::select: ") + hipGetErrorString(e));
-    return PCD_OK;
-}
-
 // Anchored K1 (seeded, list cap K <= 32, KA = 2K): the anchor test for every active row, then the re-anchoring
 // search (pcd_qknn.h) of the rows that failed it -- or of every row when there are no anchors (of this KA) yet --
 // and the exact-key wave search (pcd_wknn.h) for the few rows it spills.
-#ifndef PCD_RQ_Q
-#define PCD_RQ_Q 0             // steady re-anchoring: queries per wave sharing one scan (0: k_knn_requery, one)
-#endif
-#ifndef PCD_RQ_WD
-#define PCD_RQ_WD PCD_RQ_W     // lanes per query of the one-query dense launch (PCD_DENSE_Q = 0)
-#endif
 #ifndef PCD_RQ_RDENSE
 #define PCD_RQ_RDENSE 1.1f   // first iteration at 10M: 1.45 35.3 ms, 1.3 31.7, 1.2 29.7 (16-point cells); 1.2 26.0-26.7, 1.1 24.3 (32-point cells)
 #endif
 #ifndef PCD_RQ_GRID
 #define PCD_RQ_GRID 8192     // steady re-anchoring blocks (A/B at 10M: 4096 / 8192 / 16384 -> requery 1.23 / 1.18 / 1.17 ms)
-#endif
-#ifndef PCD_REDO_COMPACT
-#define PCD_REDO_COMPACT 1   // the redo list by k_compact_fail (one atomic per 4,096 rows); 0: rocprim::select (row order)
-#endif
-#ifndef PCD_NVT1_OVERLAP
-#define PCD_NVT1_OVERLAP 0   // measured: the side-stream NVT1 slows the re-anchoring more than it hides
 #endif
 static const Band kNoBand{Cover{{1.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, nullptr};
 static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int K, hipStream_t st,
@@ -1268,7 +1081,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     const int kstore = std::max(p->k, p->k_update);
     const int KA = 2 * K;
     if (!dn->anc) {
-        if (hipMalloc(&dn->anc, N * sizeof(float4)) != hipSuccess ||
+        if (hipMalloc(&dn->anc, N * sizeof(float4)) != hipSuccess || hipMalloc(&dn->ak1, N * sizeof(float)) != hipSuccess ||
             hipMalloc(&dn->alist, (int64_t)2 * knn_cap(dn->kcap) * N * sizeof(int32_t)) != hipSuccess ||
             hipMalloc(&dn->redo, N * sizeof(int32_t)) != hipSuccess ||
             hipMalloc(&dn->spill, N * sizeof(int32_t)) != hipSuccess || hipMalloc(&dn->fail, N) != hipSuccess ||
@@ -1285,81 +1098,48 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     unsigned* redo_cnt = &dn->rqs->redo_cnt;
     unsigned* spill_cnt = &dn->rqs->spill_cnt;
     const dim3 blk(256), grd((unsigned)cdiv(rm.nq, 256));
-    const dim3 grd_rq((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), dense ? 16384 : PCD_RQ_GRID));
+    const dim3 grd_rq((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), PCD_RQ_GRID));
     const dim3 grd_wave((unsigned)std::min<int64_t>(cdiv(rm.nq, 4), PCD_REDO_GRID));
-    const dim3 grd_dq((unsigned)std::min<int64_t>(cdiv(rm.nq, 4 * std::max(PCD_DENSE_Q, 1)), 16384));
+    const dim3 grd_dq((unsigned)std::min<int64_t>(cdiv(rm.nq, 4 * PCD_DENSE_Q), 16384));
     const dim3 grd_anc((unsigned)cdiv(rm.nq, kAnchorBS)), grd_cmp((unsigned)cdiv(rm.nq, kCompactBS * kCompactPer));
-    int rc = PCD_OK;
-    // Dense (no anchors): every row is re-anchored, then NVT1 runs over all rows.  Seeded: the anchor test, then
-    // NVT1 of the certified rows on the side stream while this stream re-anchors the others (latency-bound wave
-    // searches beside VALU-bound lane work), then NVT1 of the re-anchored rows, then the join.
-    // (never under the slab iteration -- its NVT1 waits for the halo exchange and marks the band, which the side
-    // stream's k_nvt1 / k_nvt1_list do not -- nor for the CPSD driver's lists-only K1)
-    const bool overlap = !dense && PCD_NVT1_OVERLAP && dn->nvt1_on && !before_nvt1 && !band.flag;
-    if (overlap && !dn->side) {
-        PCD_HIP(hipStreamCreateWithFlags(&dn->side, hipStreamNonBlocking));
-        PCD_HIP(hipEventCreateWithFlags(&dn->fork, hipEventDisableTiming));
-        PCD_HIP(hipEventCreateWithFlags(&dn->join, hipEventDisableTiming));
-    }
-    const dim3 grd_list((unsigned)std::min<int64_t>(cdiv(rm.nq, 256), 1024));
+    // Dense (no anchors): every row is re-anchored (PCD_DENSE_Q queries per wave sharing one scan), then NVT1 runs
+    // over all rows.  Seeded: the anchor test, the redo list of its failures, their re-anchoring search, then NVT1
+    // over all rows.  (A side-stream NVT1 of the certified rows beside the search, and two steady queries per wave,
+    // were measured slower: DESIGN.md §3 tried table.)
     const dim3 blk_nvt(kNvtBS), grd_nvt((unsigned)cdiv(rm.nq, kNvtBS));
 #define PCD_K1A(C)                                                                                                     \
     case C:                                                                                                            \
         if (dense) {                                                                                                   \
             if (ev) PCD_HIP(hipEventRecord(ev[1], st));                                                                \
-            if (PCD_DENSE_Q > 0 && PCD_DENSE_PRE) {                                                                    \
-                /* the radii by a lane-per-row pass, into the redo list (idle until the steady iterations) */        \
-                /* (PCD_DENSE_PRE 2: and the query boxes, into f_n -- rewritten by NVT1 after the search) */          \
-                float* rpre = reinterpret_cast<float*>(dn->redo);                                                      \
-                uint4* bpre = PCD_DENSE_PRE >= 2 && !rm.rows ? reinterpret_cast<uint4*>(dn->fn) : nullptr;             \
-                hipLaunchKernelGGL(k_dense_radius, grd, blk, 0, st, gv, P, rm, PCD_RQ_RDENSE, rpre, bpre);             \
-                hipLaunchKernelGGL((k_knn_dense_q<2 * C, (PCD_DENSE_Q > 0 ? PCD_DENSE_Q : 1)>), grd_dq, blk, 0, st, gv, P, N, rm, \
-                                   kstore, PCD_RQ_RDENSE, dn->anc, dn->alist, dn->idx, dn->spill, spill_cnt, nullptr,   \
-                                   nullptr, rpre, bpre);                                                               \
-            } else if (PCD_DENSE_Q > 0)                                                                                \
-                hipLaunchKernelGGL((k_knn_dense_q<2 * C, (PCD_DENSE_Q > 0 ? PCD_DENSE_Q : 1)>), grd_dq, blk, 0, st, gv, P, N, rm, \
-                                   kstore, PCD_RQ_RDENSE, dn->anc, dn->alist, dn->idx, dn->spill, spill_cnt);          \
-            else                                                                                                       \
-                hipLaunchKernelGGL((k_knn_requery<2 * C, true, PCD_RQ_WD>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, PCD_RQ_RDENSE, \
-                                   dn->anc, dn->alist, dn->idx, nullptr, nullptr, dn->spill, spill_cnt);               \
+            /* the radii by a lane-per-row pass (k_dense_radius), into the redo list (idle until the steady */      \
+            /* iterations), and the query boxes into f_n (rewritten by NVT1 after the search; not when K1 runs */     \
+            /* lists only): first iteration 21.1 -> 19.6 -> 19.1 ms at 10M */                                       \
+            float* rpre = reinterpret_cast<float*>(dn->redo);                                                          \
+            uint4* bpre = !rm.rows && dn->nvt1_on ? reinterpret_cast<uint4*>(dn->fn) : nullptr;                        \
+            hipLaunchKernelGGL(k_dense_radius, grd, blk, 0, st, gv, P, rm, PCD_RQ_RDENSE, rpre, bpre);                 \
+            hipLaunchKernelGGL((k_knn_dense_q<2 * C, PCD_DENSE_Q>), grd_dq, blk, 0, st, gv, P, N, rm, kstore,          \
+                               dn->anc, dn->ak1, dn->alist, dn->idx, dn->spill, spill_cnt, rpre, bpre);                \
         } else {                                                                                                       \
             hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd_anc, dim3(kAnchorBS), 0, st, gv, P, N, rm, kstore,        \
-                               dn->anc, dn->alist, dn->idx, dn->fail);                                                 \
-            if (PCD_REDO_COMPACT && !overlap)                                                                          \
-                hipLaunchKernelGGL(k_compact_fail, grd_cmp, dim3(kCompactBS), 0, st, dn->fail, rm, dn->redo, redo_cnt); \
-            else if ((rc = select_rows(dn, rm, dn->redo, redo_cnt, st)) != PCD_OK) return rc;                          \
-            if (overlap) {                                                                                             \
-                PCD_HIP(hipEventRecord(dn->fork, st));                                                                 \
-                PCD_HIP(hipStreamWaitEvent(dn->side, dn->fork, 0));                                                    \
-                hipLaunchKernelGGL((k_nvt1<C, false>), grd_nvt, blk_nvt, 0, dn->side, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,   \
-                                   p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, dn->fail, kNoBand); \
-                PCD_HIP(hipEventRecord(dn->join, dn->side));                                                           \
-            }                                                                                                          \
+                               dn->anc, dn->ak1, dn->alist, dn->idx, dn->fail);                                        \
+            hipLaunchKernelGGL(k_compact_fail, grd_cmp, dim3(kCompactBS), 0, st, dn->fail, rm, dn->redo, redo_cnt);    \
             if (ev) PCD_HIP(hipEventRecord(ev[1], st));                                                                \
-            if (PCD_RQ_Q > 0)                                                                                          \
-                hipLaunchKernelGGL((k_knn_dense_q<2 * C, (PCD_RQ_Q > 0 ? PCD_RQ_Q : 1), true>), grd_rq, blk, 0, st, gv, P, N, \
-                                   rm, kstore, 0.f, dn->anc, dn->alist, dn->idx, dn->spill, spill_cnt, dn->redo, redo_cnt); \
-            else                                                                                                       \
-                hipLaunchKernelGGL((k_knn_requery<2 * C, false>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, 0.f, dn->anc, \
-                                   dn->alist, dn->idx, dn->redo, redo_cnt, dn->spill, spill_cnt);                     \
+            hipLaunchKernelGGL((k_knn_requery<2 * C>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, dn->anc, dn->ak1,     \
+                               dn->alist, dn->idx, dn->redo, redo_cnt, dn->spill, spill_cnt);                          \
         }                                                                                                              \
         if (ev) PCD_HIP(hipEventRecord(ev[2], st));                                                                    \
         hipLaunchKernelGGL((k_knn_redo_wave<2 * C, false>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,       \
-                           dn->alist, dn->idx, dn->spill, spill_cnt, dn->err);                                         \
+                           dn->ak1, dn->alist, dn->idx, dn->spill, spill_cnt, dn->err);                                \
         if (ev) PCD_HIP(hipEventRecord(ev[3], st));                                                                    \
         if (before_nvt1) PCD_HIP(hipStreamWaitEvent(st, before_nvt1, 0));                                              \
-        if (overlap) {                                                                                                 \
-            hipLaunchKernelGGL((k_nvt1_list<C>), grd_list, blk, 0, st, gv, P, dn->nrm, dn->idx, N, p->k, kstore,       \
-                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->redo, redo_cnt);                 \
-            PCD_HIP(hipStreamWaitEvent(st, dn->join, 0));                                                              \
-        } else if (!dn->nvt1_on) {                                                                                     \
+        if (!dn->nvt1_on) {                                                                                            \
             /* the kNN lists only (the CPSD driver's update selection, pcd_cpsd.h) */                                   \
         } else if (dn->unit_nrm) {                                                                                     \
             hipLaunchKernelGGL((k_nvt1<C, true>), grd_nvt, blk_nvt, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,       \
-                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, nullptr, band);         \
+                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, band);                  \
         } else {                                                                                                       \
             hipLaunchKernelGGL((k_nvt1<C, false>), grd_nvt, blk_nvt, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,      \
-                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, nullptr, band);         \
+                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, band);                  \
         }                                                                                                              \
         break;
     switch (K) {
@@ -1445,7 +1225,7 @@ static int stage_sum(pcd_denoiser* dn, const pcd_denoise_params* p, int ph, doub
 
 static int stage_centre(pcd_denoiser* dn, int ph, const double* red4, hipStream_t st) {
     // (the pruning needs this phase's partials: stage_sum of the same phase on the same positions)
-    const bool prune = PCD_MAXDIST_PRUNE && dn->part_ph == ph;
+    const bool prune = dn->part_ph == ph;   // the max-distance pass skips the blocks that cannot hold the maximum
     hipLaunchKernelGGL(k_centre, dim3(1), dim3(256), 0, st, red4, dn->gscal + 4 * ph, prune ? dn->part : nullptr,
                        kNumPart);
     dn->scan_ph = prune ? ph : -1;
@@ -1555,7 +1335,7 @@ int pcd_denoiser_create(const pcd_grid* g, int k_max, pcd_denoiser** out) {
               hipMalloc(&dn->part, kNumPart * sizeof(RedC)) == hipSuccess &&
               hipMalloc(&dn->red, 16 * sizeof(double)) == hipSuccess &&
               hipMalloc(&dn->gscal, 16 * sizeof(float)) == hipSuccess &&
-              hipMalloc(&dn->err, sizeof(int)) == hipSuccess && hipMemset(dn->err, 0, sizeof(int)) == hipSuccess &&
+              hipMalloc(&dn->err, 4 * sizeof(int)) == hipSuccess && hipMemset(dn->err, 0, 4 * sizeof(int)) == hipSuccess &&
               hipMemset(dn->cls, 0xFF, N) == hipSuccess;
     if (!ok) {
         pcd_denoiser_destroy(dn);
@@ -1573,11 +1353,8 @@ int pcd_denoiser_destroy(pcd_denoiser* dn) {
     (void)hipFree(dn->xrad);
     (void)hipFree(dn->edge); (void)hipFree(dn->orig); (void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part);
     (void)hipFree(dn->red); (void)hipFree(dn->gscal); (void)hipFree(dn->err);
-    (void)hipFree(dn->anc); (void)hipFree(dn->alist); (void)hipFree(dn->redo); (void)hipFree(dn->spill);
-    (void)hipFree(dn->rqs); (void)hipFree(dn->fail); (void)hipFree(dn->sel_tmp); (void)hipFree(dn->probe);
-    if (dn->side) (void)hipStreamDestroy(dn->side);
-    if (dn->fork) (void)hipEventDestroy(dn->fork);
-    if (dn->join) (void)hipEventDestroy(dn->join);
+    (void)hipFree(dn->anc); (void)hipFree(dn->ak1); (void)hipFree(dn->alist); (void)hipFree(dn->redo); (void)hipFree(dn->spill);
+    (void)hipFree(dn->rqs); (void)hipFree(dn->fail); (void)hipFree(dn->probe);
     for (auto e : dn->ev) (void)hipEventDestroy(e);
     delete dn;
     return PCD_OK;
@@ -1707,6 +1484,17 @@ int pcd_denoiser_check(pcd_denoiser* dn, void* stream) {
     return PCD_OK;
 }
 
+int pcd_denoiser_coverage_excess(pcd_denoiser* dn, float* band_excess, float* sphere_ratio, void* stream) {
+    PCD_CHECK_ARG(dn && band_excess && sphere_ratio, "null argument");
+    if (settle(dn, as_stream(stream)) != PCD_OK) return PCD_ERR_HIP;
+    int w[4];
+    PCD_HIP(hipMemcpyAsync(w, dn->err, sizeof w, hipMemcpyDeviceToHost, as_stream(stream)));
+    PCD_HIP(hipStreamSynchronize(as_stream(stream)));
+    *band_excess = (w[0] & 4) ? __builtin_bit_cast(float, w[1]) : 0.f;
+    *sphere_ratio = (w[0] & 8) ? __builtin_bit_cast(float, w[2]) : 0.f;
+    return PCD_OK;
+}
+
 int pcd_denoiser_status(pcd_denoiser* dn, int* bits, void* stream) {
     PCD_CHECK_ARG(dn && bits, "null argument");
     // (an exchange still in flight finishes first: a collective the caller issues next on its comm -- the slab
@@ -1733,17 +1521,6 @@ int pcd_denoiser_reset_seed(pcd_denoiser* dn) {
     dn->anchor_ka = 0;
     return PCD_OK;
 }
-
-#ifdef PCD_WKNN_STATS
-int pcd_debug_wstats(unsigned long long* out8, int reset) {
-    PCD_HIP(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_wstats), 8 * sizeof(unsigned long long)));
-    if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        PCD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wstats), z, sizeof z));
-    }
-    return PCD_OK;
-}
-#endif
 
 int pcd_denoiser_anchor_stats(pcd_denoiser* dn, int64_t* redo_rows, void* stream) {
     PCD_CHECK_ARG(dn && redo_rows, "null argument");
@@ -1857,7 +1634,7 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
         if (ev) PCD_HIP(hipEventRecord(ev[5], st));
         // copy-free phases when three Gauss-Seidel phases move the three classes of every row once each and only the
         // first phase reduces globally (its reductions read the positions before any phase)
-        const bool split = PCD_PHASE_SPLIT && !p->jacobi && !dn->rows && p->nphases == 3 &&
+        const bool split = !p->jacobi && !dn->rows && p->nphases == 3 &&
                            ((1u << p->phase_class[0]) | (1u << p->phase_class[1]) | (1u << p->phase_class[2])) == 7u &&
                            !phase_is_global(p, 1) && !phase_is_global(p, 2);
         uint32_t moved = 0;

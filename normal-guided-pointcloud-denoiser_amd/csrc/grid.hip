@@ -121,16 +121,9 @@ __global__ void k_brick_flags(const unsigned long long* __restrict__ keys, int64
     if (r < n) flag[r] = (r == 0 || (keys[r] >> 6) != (keys[r - 1] >> 6)) ? 1u : 0u;
 }
 
-// the octant (top sub-cell level) of every sorted row, before the sub bits are shifted out of the keys
-__global__ void k_row_octant(const unsigned long long* __restrict__ keys, int64_t n, int sub, uint8_t* __restrict__ oct) {
-    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (r < n) oct[r] = (uint8_t)((keys[r] >> (3 * (sub - 1))) & 7);
-}
-
 // bidx = inclusive scan of the brick-start flags: row r lies in brick bidx[r] - 1 (bricks numbered in Morton order)
 __global__ void k_insert(const unsigned long long* __restrict__ keys, const uint32_t* __restrict__ bidx, int64_t n,
-                         HashSlot* table, int hbits, unsigned long long mask, uint2* __restrict__ cellr,
-                         const uint8_t* __restrict__ oct8, uint2* __restrict__ coct) {
+                         HashSlot* table, int hbits, unsigned long long mask, uint2* __restrict__ cellr) {
     const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (r >= n) return;
     const unsigned long long key = keys[r];
@@ -139,20 +132,6 @@ __global__ void k_insert(const unsigned long long* __restrict__ keys, const uint
     while (end < n && keys[end] == key) ++end;
     const uint32_t b = bidx[r] - 1u;
     cellr[(uint64_t)b * 64 + (key & 63)] = make_uint2((uint32_t)r, (uint32_t)end);
-    if (coct) {
-        // octant starts: rows are in octant order inside the cell (the octant is the top sub-cell Morton digit)
-        uint2 o = make_uint2(0u, 0u);
-        if (end - r < 256) {
-            uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (int64_t t = r; t < end; ++t) ++c[oct8[t]];
-            uint32_t run = 0, bytes[8];
-            for (int k = 0; k < 8; ++k) { bytes[k] = run; run += c[k]; }
-            bytes[0] = 1u;                            // valid
-            o.x = bytes[0] | (bytes[1] << 8) | (bytes[2] << 16) | (bytes[3] << 24);
-            o.y = bytes[4] | (bytes[5] << 8) | (bytes[6] << 16) | (bytes[7] << 24);
-        }
-        coct[(uint64_t)b * 64 + (key & 63)] = o;
-    }
     if (r != 0 && (keys[r - 1] >> 6) == (key >> 6)) return;   // one thread per brick inserts it
     const unsigned long long bkey = key >> 6;
     unsigned long long slot = hash_slot(bkey, hbits);
@@ -448,9 +427,6 @@ int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, const fl
     if (rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, keys2, vals, g->perm, (size_t)n, 0u, 63u, st) != hipSuccess) {
         free_tmp(); cleanup(); return fail(PCD_ERR_HIP, "rocprim::radix_sort_pairs failed");
     }
-    // octants of the sorted rows into the pre-sort key buffer's upper half (its lower half becomes bidx below)
-    uint8_t* oct8 = (PCD_RQ_OCT && sub) ? reinterpret_cast<uint8_t*>(keys) + n * 4 : nullptr;
-    if (oct8) hipLaunchKernelGGL(k_row_octant, grd, blk, 0, st, keys2, n, sub, oct8);
     if (sub) hipLaunchKernelGGL(k_key_shift, grd, blk, 0, st, keys2, n, 3 * sub);
     hipLaunchKernelGGL(k_gather_sorted, grd, blk, 0, st, xyz, g->perm, n, g->pts);
     hipLaunchKernelGGL(k_sentinel, dim3(1), dim3(64), 0, st, g->pts + n);
@@ -474,12 +450,6 @@ int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, const fl
     }
     (void)hipMemsetAsync(g->table, 0xFF, g->slots * sizeof(HashSlot), st);
     (void)hipMemsetAsync(g->cellr, 0, g->bricks * 64 * sizeof(uint2), st);
-    if (oct8) {
-        if (hipMalloc(&g->coct, g->bricks * 64 * sizeof(uint2)) != hipSuccess) {
-            free_tmp(); cleanup(); return fail(PCD_ERR_OOM, "octant index");
-        }
-        (void)hipMemsetAsync(g->coct, 0, g->bricks * 64 * sizeof(uint2), st);
-    }
     hipLaunchKernelGGL(k_brick_flags, grd, blk, 0, st, keys2, n, bflag);
     size_t scan_bytes = 0;
     (void)rocprim::inclusive_scan(nullptr, scan_bytes, bflag, bidx, (size_t)n, rocprim::plus<uint32_t>(), st);
@@ -492,17 +462,16 @@ int pcd_grid_build(const float* xyz, int64_t n, int k_hint, float cell, const fl
         free_tmp(); cleanup(); return fail(PCD_ERR_HIP, "rocprim::inclusive_scan failed");
     }
     hipLaunchKernelGGL(k_insert, grd, blk, 0, st, keys2, bidx, n, g->table, hbits, (unsigned long long)(g->slots - 1),
-                       g->cellr, oct8, g->coct);
+                       g->cellr);
     e = hipStreamSynchronize(st);
     free_tmp();
     if (e != hipSuccess) { cleanup(); return fail(PCD_ERR_HIP, std::string("grid hash: ") + hipGetErrorString(e)); }
     v.pts = g->pts;
     v.table = g->table;
     v.cells = g->cellr;
-    v.oct = g->coct;
     {
         // a row's key comes from fp32 (p - o) * inv_h: its true position can sit a few ulps of |p|, |o| and of the
-        // cell coordinate (times h) outside the box its cell / octant index describes
+        // cell coordinate (times h) outside the box its cell describes
         const double amax = std::max({std::fabs((double)mn[0]), std::fabs((double)mn[1]), std::fabs((double)mn[2]),
                                       std::fabs((double)mx[0]), std::fabs((double)mx[1]), std::fabs((double)mx[2])});
         const double dmax = std::max({v.dx, v.dy, v.dz});
@@ -520,7 +489,7 @@ int pcd_grid_destroy(pcd_grid* g) {
     (void)hipFree(g->perm);
     (void)hipFree(g->table);
     (void)hipFree(g->cellr);
-    (void)hipFree(g->coct);
+
     delete g;
     return PCD_OK;
 }

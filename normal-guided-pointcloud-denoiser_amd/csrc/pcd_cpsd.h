@@ -27,9 +27,6 @@ static constexpr int kCpsdBS = 128;
 #define PCD_CPSD_CELLS 4
 #endif
 static constexpr int kCpsdCells = PCD_CPSD_CELLS;   // box cells looked up together by a lane
-#ifndef PCD_CPSD_NET
-#define PCD_CPSD_NET 1
-#endif
 #ifndef PCD_CPSD_ROWS
 #define PCD_CPSD_ROWS 8
 #endif
@@ -186,13 +183,10 @@ __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __res
         m = cap;
     }
     // ascending original index: scipy's per-query order, the order the reference's scatter sums in
-#if defined(PCD_EXP_CPSD) && PCD_EXP_CPSD >= 1      // timing experiment: no sort (sums in scan order: results differ)
-    if (m < 0)
-#endif
     {
-#if PCD_CPSD_NET
     // the LDS slots by a fixed network in registers (no chain of dependent LDS round trips; unused slots padded with
-    // the largest key), then the few overflow members (past L) inserted one by one
+    // the largest key), then the few overflow members (past L) inserted one by one (an LDS insertion sort over every
+    // member: 601 -> 429 us at 1M points)
     {
         const int m0 = min(m, L);
         uint32_t v[L];
@@ -204,9 +198,6 @@ __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __res
             if (t < m0) S.lds[t * S.bs] = v[t];
     }
     for (int a = L; a < m; ++a) {
-#else
-    for (int a = 1; a < m; ++a) {
-#endif
         const uint32_t k = S.get(a);
         int b = a - 1;
         for (; b >= 0; --b) {
@@ -221,9 +212,6 @@ __global__ __launch_bounds__(BS) void k_cpsd_nvt(GridView g, const float4* __res
     for (int t = 0; t < m; ++t) S.glb[t * rm.nq] = (uint32_t)inv[S.get(t)];
     const float4 n4 = nrm[i];
     const Vec3 ni = v3(n4.x, n4.y, n4.z);
-#if defined(PCD_EXP_CPSD) && PCD_EXP_CPSD >= 2      // timing experiment: no tensor / eigh (f_n = n)
-    if (m >= 0) { fn[i] = n4; return; }
-#endif
     const Sym3 T = nvt_normal_tensor(Rows4{nrm}, ni, m, RowNb{rows + t0, rm.nq}, rho);
     float w[3], V[3][3];
     eigh3(T, w, V);

@@ -78,22 +78,10 @@ struct RowMap {
 struct Sym3 { float a00, a01, a02, a11, a12, a22; };
 
 namespace lapack {
-// PCD_EIGH_FAST (experiment): the hardware reciprocal / square-root estimates (~1 ulp) in place of IEEE division and
-// sqrt inside the solver; the default build keeps LAPACK's IEEE arithmetic.
-PCD_DEV float ldiv(float a, float b) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(PCD_EIGH_FAST)
-    return a * __builtin_amdgcn_rcpf(b);
-#else
-    return a / b;
-#endif
-}
-PCD_DEV float lsqrt(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(PCD_EIGH_FAST)
-    return __builtin_amdgcn_sqrtf(x);
-#else
-    return sqrtf(x);
-#endif
-}
+// LAPACK's IEEE division and square root (the hardware estimates flip eigenvector signs on 0.2-0.4 % of the fandisk
+// points: measured)
+PCD_DEV float ldiv(float a, float b) { return a / b; }
+PCD_DEV float lsqrt(float x) { return sqrtf(x); }
 static constexpr float kEps = 5.9604644775390625e-08f;      // slamch('E') = 2^-24
 static constexpr float kSafmin = 1.17549435e-38f;          // slamch('S')
 static constexpr float kSafmn2 = 4.4408920985006262e-16f;  // 2^-51 (slartg scaling bounds)
@@ -372,170 +360,9 @@ PCD_DEV void ssteqr3(float d[3], float e[2], float Z[3][3]) {
         }
     }
 }
-#ifdef PCD_EIGH_GENERIC
-// ssteqr(compz='I') for n = 3 written as LAPACK's general loop (runtime block indices).  Kept only as the
-// reference for tools/eigh_equiv.cpp, which checks ssteqr3 below against it bit for bit.
-PCD_DEV void ssteqr3_generic(float d[3], float e[2], float Z[3][3]) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) Z[i][j] = (i == j) ? 1.f : 0.f;
-    const float eps2 = kEps * kEps;
-    const int nmaxit = 3 * 30;
-    int jtot = 0;
-    int l1 = 0;
-    while (l1 <= 2) {
-        if (l1 > 0) e[l1 - 1] = 0.f;
-        int m = 2;
-        for (int mm = l1; mm < 2; ++mm) {
-            const float tst = fabsf(e[mm]);
-            if (tst == 0.f) { m = mm; break; }
-            if (tst <= (sqrtf(fabsf(d[mm])) * sqrtf(fabsf(d[mm + 1]))) * kEps) { e[mm] = 0.f; m = mm; break; }
-        }
-        int l = l1;
-        const int lsv = l;
-        int lend = m;
-        const int lendsv = lend;
-        l1 = m + 1;
-        if (lend == l) continue;
-        float anorm = 0.f;
-        for (int i = l; i <= lend; ++i) anorm = fmaxf(anorm, fabsf(d[i]));
-        for (int i = l; i < lend; ++i) anorm = fmaxf(anorm, fabsf(e[i]));
-        if (anorm == 0.f) continue;
-        const float sc = block_scale(anorm);
-        if (sc != 1.f) {
-            for (int i = l; i <= lend; ++i) d[i] *= sc;
-            for (int i = l; i < lend; ++i) e[i] *= sc;
-        }
-        if (fabsf(d[lend]) < fabsf(d[l])) { lend = lsv; l = lendsv; }
-        if (lend > l) {
-            // ---------------- QL iteration
-            for (;;) {
-                int mq = lend;
-                if (l != lend) {
-                    for (int mm = l; mm < lend; ++mm) {
-                        const float tst = fabsf(e[mm]) * fabsf(e[mm]);
-                        if (tst <= (eps2 * fabsf(d[mm])) * fabsf(d[mm + 1]) + kSafmin) { mq = mm; break; }
-                    }
-                }
-                if (mq < lend) e[mq] = 0.f;
-                float p = d[l];
-                if (mq == l) {
-                    d[l] = p; ++l;
-                    if (l <= lend) continue;
-                    break;
-                }
-                if (mq == l + 1) {
-                    float rt1, rt2, c, s;
-                    slaev2(d[l], e[l], d[l + 1], rt1, rt2, c, s);
-                    rot_cols(Z, l, c, s);
-                    d[l] = rt1; d[l + 1] = rt2; e[l] = 0.f; l += 2;
-                    if (l <= lend) continue;
-                    break;
-                }
-                if (jtot == nmaxit) break;
-                ++jtot;
-                float g = (d[l + 1] - p) / (2.f * e[l]);
-                float r = slapy2(g, 1.f);
-                g = d[mq] - p + (e[l] / (g + fsign(r, g)));
-                float s = 1.f, c = 1.f;
-                p = 0.f;
-                float wc[2], ws[2];
-                for (int i = mq - 1; i >= l; --i) {
-                    const float f = s * e[i], b = c * e[i];
-                    slartg(g, f, c, s, r);
-                    if (i != mq - 1) e[i + 1] = r;
-                    g = d[i + 1] - p;
-                    r = (d[i] - g) * s + 2.f * c * b;
-                    p = s * r;
-                    d[i + 1] = g + p;
-                    g = c * r - b;
-                    wc[i - l] = c; ws[i - l] = -s;
-                }
-                for (int j = mq - 1; j >= l; --j) rot_cols(Z, j, wc[j - l], ws[j - l]);   // slasr 'B'
-                d[l] = d[l] - p;
-                e[l] = g;
-            }
-        } else {
-            // ---------------- QR iteration
-            for (;;) {
-                int mq = lend;
-                if (l != lend) {
-                    for (int mm = l; mm > lend; --mm) {
-                        const float tst = fabsf(e[mm - 1]) * fabsf(e[mm - 1]);
-                        if (tst <= (eps2 * fabsf(d[mm])) * fabsf(d[mm - 1]) + kSafmin) { mq = mm; break; }
-                    }
-                }
-                if (mq > lend) e[mq - 1] = 0.f;
-                float p = d[l];
-                if (mq == l) {
-                    d[l] = p; --l;
-                    if (l >= lend) continue;
-                    break;
-                }
-                if (mq == l - 1) {
-                    float rt1, rt2, c, s;
-                    slaev2(d[l - 1], e[l - 1], d[l], rt1, rt2, c, s);
-                    rot_cols(Z, l - 1, c, s);
-                    d[l - 1] = rt1; d[l] = rt2; e[l - 1] = 0.f; l -= 2;
-                    if (l >= lend) continue;
-                    break;
-                }
-                if (jtot == nmaxit) break;
-                ++jtot;
-                float g = (d[l - 1] - p) / (2.f * e[l - 1]);
-                float r = slapy2(g, 1.f);
-                g = d[mq] - p + (e[l - 1] / (g + fsign(r, g)));
-                float s = 1.f, c = 1.f;
-                p = 0.f;
-                float wc[2], ws[2];
-                for (int i = mq; i <= l - 1; ++i) {
-                    const float f = s * e[i], b = c * e[i];
-                    slartg(g, f, c, s, r);
-                    if (i != mq) e[i - 1] = r;
-                    g = d[i] - p;
-                    r = (d[i + 1] - g) * s + 2.f * c * b;
-                    p = s * r;
-                    d[i] = g + p;
-                    g = c * r - b;
-                    wc[i - mq] = c; ws[i - mq] = s;
-                }
-                for (int j = mq; j <= l - 1; ++j) rot_cols(Z, j, wc[j - mq], ws[j - mq]);   // slasr 'F'
-                d[l] = d[l] - p;
-                e[l - 1] = g;
-            }
-        }
-        if (sc != 1.f) {
-            const float us = block_unscale(anorm);
-            for (int i = lsv; i <= lendsv; ++i) d[i] *= us;
-            for (int i = lsv; i < lendsv; ++i) e[i] *= us;
-        }
-        if (jtot >= nmaxit) break;
-    }
-    // selection sort, ascending (swaps columns of Z)
-    for (int ii = 1; ii < 3; ++ii) {
-        const int i = ii - 1;
-        int k = i;
-        float p = d[i];
-        for (int j = ii; j < 3; ++j)
-            if (d[j] < p) { k = j; p = d[j]; }
-        if (k != i) {
-            d[k] = d[i]; d[i] = p;
-#pragma unroll
-            for (int r = 0; r < 3; ++r) { const float t = Z[r][i]; Z[r][i] = Z[r][k]; Z[r][k] = t; }
-        }
-    }
-}
-#endif
 }  // namespace lapack
 
-template <int IMPL = 0>   // IMPL 1 (tools/eigh_equiv.cpp only): LAPACK's general ssteqr loop
 PCD_DEV void eigh3(Sym3 A, float w[3], float V[3][3]) {
-#ifdef PCD_EXP_NOEIGH     // experiment builds only: timing without the eigen-solver (results wrong)
-    w[0] = A.a00; w[1] = A.a11; w[2] = A.a22;
-    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) V[r][c] = r == c ? A.a01 : A.a12;
-    return;
-#endif
     using namespace lapack;
     // ssyevd's scaling: a matrix whose largest entry lies outside [rmin, rmax] is scaled into range first (slascl: one
     // multiplication by sigma for every sigma reachable here) and the eigenvalues are scaled back by 1/sigma
@@ -573,9 +400,6 @@ PCD_DEV void eigh3(Sym3 A, float w[3], float V[3][3]) {
     float d[3] = {A.a00, a22, a33};
     float e[2] = {e1, a32};
     float Z[3][3];
-#ifdef PCD_EIGH_GENERIC
-    if (IMPL == 1) ssteqr3_generic(d, e, Z); else
-#endif
     ssteqr3(d, e, Z);
     // sormtr: Z := H(1) Z on rows 2..3 (slarf: w = Zᵀv unfused, then Z -= tau v wᵀ fused, as mkl_lapack_sormtr)
     if (tau != 0.f) {
@@ -721,23 +545,23 @@ PCD_DEV Vec3 vu_smooth(const float w[3], const float V[3][3], Vec3 n, float tau,
 // divergence.  Eigenvalue error ~1e-7 of the trace (the tests' bound for eigenvalues is 2e-6).
 // On the device the rotation is built from the hardware reciprocal / square-root estimates (~1 ulp): any (c, s)
 // with c² + s² = 1 to rounding keeps the similarity orthogonal, and the off-diagonal still vanishes to rounding
-// after the fixed sweeps, so only the last bits of the eigenvalues change (PCD_NVT2_IEEE: the IEEE operations).
+// after the fixed sweeps, so only the last bits of the eigenvalues change (the host build: the IEEE operations).
 PCD_DEV float jrcp(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(PCD_NVT2_IEEE)
+#if defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_rcpf(x);
 #else
     return 1.f / x;
 #endif
 }
 PCD_DEV float jsqrt(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(PCD_NVT2_IEEE)
+#if defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_sqrtf(x);
 #else
     return sqrtf(x);
 #endif
 }
 PCD_DEV float jrsq(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(PCD_NVT2_IEEE)
+#if defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_rsqf(x);
 #else
     return 1.f / sqrtf(x);
@@ -766,17 +590,12 @@ PCD_DEV void jacobi_rot(float (&a)[3][3], float (&V)[3][3]) {
     }
 }
 // Ascending eigenvalues w of T and the eigenvector y of w[0] (unit length, arbitrary sign).
-#ifndef PCD_JACOBI_SWEEPS
-#define PCD_JACOBI_SWEEPS 3   // (4 measured: NVT2 +0.014 ms, same classes in every parity test)
-#endif
-#ifndef PCD_NVT2_REFINE
-#define PCD_NVT2_REFINE 1     // smallest eigenvector re-derived as the null vector of T - λ0 I (below)
-#endif
+static constexpr int kJacobiSweeps = 3;   // (4 measured: NVT2 +0.014 ms, same classes in every parity test)
 PCD_DEV void eigh3_min(const Sym3& T, float w[3], Vec3& y) {
     float a[3][3] = {{T.a00, T.a01, T.a02}, {T.a01, T.a11, T.a12}, {T.a02, T.a12, T.a22}};
     float V[3][3] = {{1.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, {0.f, 0.f, 1.f}};
 #pragma unroll
-    for (int sweep = 0; sweep < PCD_JACOBI_SWEEPS; ++sweep) {
+    for (int sweep = 0; sweep < kJacobiSweeps; ++sweep) {
         jacobi_rot<0, 1, 2>(a, V);
         jacobi_rot<0, 2, 1>(a, V);
         jacobi_rot<1, 2, 0>(a, V);
@@ -793,7 +612,6 @@ PCD_DEV void eigh3_min(const Sym3& T, float w[3], Vec3& y) {
     cx(0, 1); cx(1, 2); cx(0, 1);
     w[0] = e[0]; w[1] = e[1]; w[2] = e[2];
     y = c[0] == 0 ? v3(V[0][0], V[1][0], V[2][0]) : c[0] == 1 ? v3(V[0][1], V[1][1], V[2][1]) : v3(V[0][2], V[1][2], V[2][2]);
-#if PCD_NVT2_REFINE
     // The rotation-accumulated vector carries the sweeps' leftover off-diagonal over the gap (~1e-6 / gap rad,
     // tests/test_gpu_stages.py); the null vector of T - λ0 I as the largest cross product of two of its rows is
     // accurate to rounding over the gap (λ0 itself is second-order accurate), as LAPACK's is.  Used where the gap
@@ -817,7 +635,6 @@ PCD_DEV void eigh3_min(const Sym3& T, float w[3], Vec3& y) {
             y = v3(x.x * inv, x.y * inv, x.z * inv);
         }
     }
-#endif
     if (!(d0 == d0 && d1 == d1 && d2 == d2)) { w[0] = w[1] = w[2] = NAN; }
 }
 

@@ -68,14 +68,6 @@ struct HashSlot {            // one occupied BRICK (4x4x4 cells): Morton brick k
 };
 static constexpr unsigned long long kEmptyKey = ~0ull;
 
-// Octant index of the cells (PCD_RQ_OCT): a cell's rows are in sub-cell Morton order, so its 8 octants (half-cells)
-// are consecutive runs; byte o (1..7) of a cell's uint2 = where octant o starts, relative to the cell's first row;
-// byte 0 = 1 when the index is valid (fewer than 256 rows).  The re-anchoring scan reads only the rows from the
-// first to the last octant its ball can reach.
-#ifndef PCD_RQ_OCT
-#define PCD_RQ_OCT 0
-#endif
-
 // Kernel-side view of a grid (passed by value).
 struct GridView {
     const float4* pts;       // snapshot, Morton-sorted, w unused
@@ -86,8 +78,7 @@ struct GridView {
     float ox, oy, oz, h, inv_h;
     int dx, dy, dz;
     int64_t n;
-    const uint2* oct;        // [bricks][64] octant starts (PCD_RQ_OCT builds; else null)
-    float slack;             // bound on how far a row can sit outside its cell / octant box (fp32 rounding of the keys)
+    float slack;             // bound on how far a row can sit outside its cell box (fp32 rounding of the keys)
 };
 
 }  // namespace pcd
@@ -100,7 +91,6 @@ struct pcd_grid {
     int32_t* perm = nullptr;   // [n] sorted rank -> original index
     pcd::HashSlot* table = nullptr;
     uint2* cellr = nullptr;    // [bricks][64]
-    uint2* coct = nullptr;     // [bricks][64] octant starts (PCD_RQ_OCT)
     int64_t slots = 0;
     int64_t bricks = 0;
     pcd::GridView view{};

@@ -83,9 +83,6 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF n
     auto body2 = [&](const Vec3 vj, const Vec3 nj) {
         const f2 dxy = f2{vj.x, vj.y} - vixy;
         const float dz = vj.z - vi.z;
-#if defined(PCD_EXP_NOVOTE)
-        const bool w = dxy.x > 0.f;
-#else
         const f2 sxy = dxy * dxy;
         const float sq = (sxy.x + sxy.y) + dz * dz;
         const f2 exy = dxy * f2{nj.x, nj.y};
@@ -109,7 +106,6 @@ PCD_DEV Sym3 nvt_tensor(P pos, Nr nrm, Vec3 vi, int cnt, Nb nb, float rho, NbF n
             c = fabsf(fminf(fmaxf(c, -1.f), 1.f));
             w = acosf(c) > rho;
         }
-#endif
         const Vec3 nw = sel3(w, nj, v3(0.f, 0.f, 0.f));
         acc0 += f2{nw.x, nw.x} * f2{nj.x, nj.y};
         acc1 += f2{nw.x, nw.y} * f2{nj.z, nj.y};

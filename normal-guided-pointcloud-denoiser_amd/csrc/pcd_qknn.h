@@ -12,8 +12,8 @@
 //     kstore + 1) has two equal quantised values at a decision point is SPILLED to the exact-key wave search
 //     (k_knn_redo_wave), so the lists stay bit-identical to it;
 //   * a full buffer is cut to the KA best the same way (the cap tightens to the largest kept exact key + 1).
-// DENSE (no anchors yet): the cap radius is r_scale · h · (16 / n)^(1/3), n = occupancy of the query's cell; a
-// query with fewer than KA points inside it is spilled (the wave search then grows its own box).
+// The first iteration (no anchors yet, k_knn_dense_q): the radius is r_scale · h · (16 / n)^(1/3), n = occupancy of
+// the query's cell; a query with too few points inside it is widened, then spilled (the wave search grows its own box).
 #pragma once
 #include "pcd_lists.h"
 #include "pcd_wknn.h"
@@ -246,22 +246,9 @@ struct RqCells {            // per-group LDS scratch for one chunk of cells
     uint32_t end_incl[kRqChunk];
     uint8_t cellof[kRqMap > 0 ? kRqMap : 4];   // cell (slot in the chunk) of each flattened candidate row
 };
-// cellof[b..e) = v: the bytes up to the first 4-byte boundary and after the last one singly (a neighbouring lane's run
-// may share those words), the whole words between as one 32-bit store each -- a quarter of the per-byte loop's trips
-// (PCD_RQ_FILL32 = 0: the per-byte loop)
-#ifndef PCD_RQ_FILL32
-#define PCD_RQ_FILL32 0      // 1: A/B at 10M, dense first anchoring 22.1 vs 21.8 ms, steady requery equal: the byte loop kept
-#endif
+// cellof[b..e) = v, a byte at a time (whole 32-bit words between the ends measured slower: DESIGN.md §3)
 PCD_DEV void fill_cellof(uint8_t* cellof, uint32_t b, uint32_t e, uint32_t v) {
-    if (PCD_RQ_FILL32) {
-        const uint32_t wb = min((b + 3u) & ~3u, e), we = max(e & ~3u, wb);
-        for (uint32_t k = b; k < wb; ++k) cellof[k] = (uint8_t)v;
-        const uint32_t v4 = v * 0x01010101u;
-        for (uint32_t k = wb; k < we; k += 4) *reinterpret_cast<uint32_t*>(cellof + k) = v4;
-        for (uint32_t k = we; k < e; ++k) cellof[k] = (uint8_t)v;
-    } else {
-        for (uint32_t k = b; k < e; ++k) cellof[k] = (uint8_t)v;
-    }
+    for (uint32_t k = b; k < e; ++k) cellof[k] = (uint8_t)v;
 }
 // Where a scan reads its cells and candidate rows from: GridSrc is the grid in global memory (brick hash probes,
 // brick cell blocks, snapshot rows; a row's rank is its index).  A source only has to resolve a lane's cells to row
@@ -269,11 +256,9 @@ PCD_DEV void fill_cellof(uint8_t* cellof, uint32_t b, uint32_t e, uint32_t v) {
 // measured this way: DESIGN §3).
 struct GridSrc {
     const GridView* g;
-    // OCT (PCD_RQ_OCT builds with an octant index): each cell's range is cut to the rows from the first to the last
-    // octant whose box (widened by the grid's slack) lies within thr (squared) of q
-    template <int CPL, bool OCT = false>
+    template <int CPL>
     PCD_DEV void ranges(const int (&cx)[CPL], const int (&cy)[CPL], const int (&cz)[CPL], const bool (&on)[CPL],
-                        uint2 (&cr)[CPL], Vec3 q = Vec3{0.f, 0.f, 0.f}, float thr = 0.f) const {
+                        uint2 (&cr)[CPL]) const {
         uint32_t slot[CPL], loc6[CPL];
         unsigned long long bkey[CPL];
 #pragma unroll
@@ -308,36 +293,6 @@ struct GridSrc {
 #pragma unroll
         for (int u = 0; u < CPL; ++u)
             cr[u] = brick[u] != ~0u ? g->cells[(uint64_t)brick[u] * 64 + loc6[u]] : make_uint2(0u, 0u);
-        if constexpr (OCT && PCD_RQ_OCT) {
-            uint2 oc[CPL];
-#pragma unroll
-            for (int u = 0; u < CPL; ++u)
-                oc[u] = brick[u] != ~0u && g->oct ? g->oct[(uint64_t)brick[u] * 64 + loc6[u]] : make_uint2(0u, 0u);
-            const float hh = 0.5f * g->h, sl = g->slack;
-#pragma unroll
-            for (int u = 0; u < CPL; ++u) {
-                if (!(oc[u].x & 1u) || cr[u].y <= cr[u].x) continue;
-                const float lx = g->ox + cx[u] * g->h, ly = g->oy + cy[u] * g->h, lz = g->oz + cz[u] * g->h;
-                float gx[2], gy[2], gz[2];
-                gx[0] = axis_gap(q.x, lx - sl, lx + hh + sl); gx[1] = axis_gap(q.x, lx + hh - sl, lx + g->h + sl);
-                gy[0] = axis_gap(q.y, ly - sl, ly + hh + sl); gy[1] = axis_gap(q.y, ly + hh - sl, ly + g->h + sl);
-                gz[0] = axis_gap(q.z, lz - sl, lz + hh + sl); gz[1] = axis_gap(q.z, lz + hh - sl, lz + g->h + sl);
-                int first = 8, last = -1;
-#pragma unroll
-                for (int o = 0; o < 8; ++o) {
-                    const float a = gx[o & 1], b = gy[(o >> 1) & 1], c = gz[o >> 2];
-                    if (a * a + b * b + c * c <= thr) { first = min(first, o); last = o; }
-                }
-                const uint32_t n = cr[u].y - cr[u].x;
-                auto start = [&](int o) -> uint32_t {
-                    if (o <= 0) return 0u;
-                    if (o >= 8) return n;
-                    return ((o < 4 ? oc[u].x : oc[u].y) >> (8 * (o & 3))) & 0xFFu;
-                };
-                const uint32_t b0 = last < 0 ? 0u : start(first), b1 = last < 0 ? 0u : start(last + 1);
-                cr[u] = make_uint2(cr[u].x + b0, cr[u].x + b1);
-            }
-        }
     }
     PCD_DEV void row(uint32_t r, float& x, float& y, float& z, uint32_t& rank) const {
         const float* pp = reinterpret_cast<const float*>(g->pts + r);
@@ -377,7 +332,7 @@ PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo
             }
         }
         uint2 cr[CPL];
-        src.template ranges<CPL, true>(cxs, cys, czs, on, cr, q, kth * 1.00001f + 1e-30f);
+        src.template ranges<CPL>(cxs, cys, czs, on, cr);
         uint32_t loc[CPL], run = 0;
 #pragma unroll
         for (int u = 0; u < CPL; ++u) {
@@ -403,9 +358,6 @@ PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo
                 fill_cellof(wc->cellof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], (uint32_t)(hl * CPL + u));
         }
         wave_sync();
-#if defined(PCD_EXP_RQ) && (PCD_EXP_RQ == 2 || PCD_EXP_RQ == 4)    // timing experiment: cell phase only (results wrong)
-        if (total != 0x7FFFFFFF) { wave_sync(); continue; }
-#endif
         for (uint32_t j0 = 0; j0 < total; j0 += W * kRqRows) {
             // room for a whole round of appends (one cut site: the sort network is inlined once)
             if (cnt > RqSurv<W>::n - W * kRqRows && !rq_cut<K, W>(buf, cnt, cap, lg)) return false;
@@ -439,13 +391,9 @@ PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo
                     const unsigned long long key2 =
                         ((unsigned long long)__float_as_uint(dist2(q, make_float4(px[u], py[u], pz[u], 0.f))) << 32) | rk[u];
                     const bool pass = j < total && key2 < cap;
-#if defined(PCD_EXP_RQ) && PCD_EXP_RQ == 3    // timing experiment: candidates and distances, no survivors (wrong)
-                    if (pass && key2 == 0ull) buf[0] = key2;
-#else
                     const unsigned long long m = lg.ballot(pass);
                     if (pass) buf[cnt + __popcll(m & ((1ull << hl) - 1ull))] = key2;
                     cnt += __popcll(m);
-#endif
                 }
             }
         }
@@ -465,11 +413,12 @@ struct RqStats { unsigned redo_cnt, spill_cnt, spill_big, spill_amb; };
 #define PCD_RQ_OCC 8
 #endif
 // The end of a re-anchoring query once its survivors are in buf[0..cnt) under cap: the exact order checks, then the
-// stored list, the anchor set (rank order) and the anchor -- or the spill list when a check fails (ok = false on
-// entry: the scan was ambiguous or found too few points).
+// stored list, the anchor set (rank order, each entry packed with its distance band, pcd_lists.h anchor_entry), its
+// (K+1)-th distance bound ak1 and the anchor -- or the spill list when a check fails (ok = false on entry: the scan
+// was ambiguous or found too few points).
 template <int KA, int W>
 PCD_DEV void rq_finish(int64_t i, Vec3 q, float r_s, int64_t N, int kstore, float4* __restrict__ anc,
-                       int32_t* __restrict__ alist, int32_t* __restrict__ idx, int32_t* __restrict__ spill,
+                       float* __restrict__ ak1, int32_t* __restrict__ alist, int32_t* __restrict__ idx, int32_t* __restrict__ spill,
                        unsigned* __restrict__ spill_cnt, unsigned long long* buf, int cnt, unsigned long long cap,
                        bool ok, bool big, const LaneGrp<W>& lg) {
     const bool partial = cnt < KA;               // (after a buffer cut cnt == KA)
@@ -503,23 +452,34 @@ PCD_DEV void rq_finish(int64_t i, Vec3 q, float r_s, int64_t N, int kstore, floa
     // whole 32-B sectors of the blocked list layout (pcd_lists.h): lanes 8b .. 8b+7 fill block b of row i
     if (e0 < kstore) idx[lpos(N, i, e0)] = r0;
     if (e1 < kstore) idx[lpos(N, i, e1)] = r1;
+    // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
+    // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))
+    const unsigned long long mx = grp_max_u64<W>(m0 > m1 ? m0 : m1);
+    const float D = partial ? r_s * (1.f - 1e-6f) : sqrtf(__uint_as_float((unsigned)(mx >> 32)));
+    // ak1: an upper bound of the (K+1)-th distance from the anchor (element K of the order; D when the set holds
+    // fewer): the anchor test gathers only the members whose distance band lies under ak1 + 2|q - a|
+    constexpr int K = KA / 2;
+    const uint32_t oK = o.at(K);                     // (a shuffle: every lane of the group executes it)
     // the anchor set is stored in RANK order (unused slots last): the anchor test ranks it by distance itself,
     // and neighbouring rows -- neighbouring lanes of its waves -- then gather nearly the same snapshot rows in the
     // same slot, i.e. the same cache lines, instead of 64 unrelated ones per gather instruction
     {
         constexpr int M = KA > W ? 2 : 1;
         uint32_t v[M];
-        v[0] = e0 < KA ? (uint32_t)r0 : 0xFFFFFFFFu;
-        if (M > 1) v[M - 1] = e1 < KA ? (uint32_t)r1 : 0xFFFFFFFFu;
-        grp_bitonic_sort32<W, M>(v, lg.hl);
+        const uint32_t sent = anchor_entry((uint32_t)N, 3.0e38f, D);   // unused slot: the +inf sentinel row
+        v[0] = e0 < KA ? (h0 ? anchor_entry((uint32_t)r0, sqrtf(__uint_as_float((unsigned)(m0 >> 32))), D) : sent)
+                       : 0xFFFFFFFFu;
+        if (M > 1)
+            v[M - 1] = e1 < KA ? (h1 ? anchor_entry((uint32_t)r1, sqrtf(__uint_as_float((unsigned)(m1 >> 32))), D) : sent)
+                               : 0xFFFFFFFFu;
+        grp_bitonic_sort32<W, M>(v, lg.hl);        // (by rank: the rank is the entry's high bits)
         if (e0 < KA) alist[lpos(N, i, e0)] = (int32_t)v[0];
         if (M > 1 && e1 < KA) alist[lpos(N, i, e1)] = (int32_t)v[M - 1];
     }
-    // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
-    // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))
-    const unsigned long long mx = grp_max_u64<W>(m0 > m1 ? m0 : m1);
-    const float D = partial ? r_s * (1.f - 1e-6f) : sqrtf(__uint_as_float((unsigned)(mx >> 32)));
-    if (lg.hl == 0) anc[i] = make_float4(q.x, q.y, q.z, D);
+    if (lg.hl == 0) {
+        anc[i] = make_float4(q.x, q.y, q.z, D);
+        ak1[i] = K < cnt ? sqrtf(__uint_as_float((unsigned)(buf[oK & 255u] >> 32))) * (1.f + 1e-5f) : D;
+    }
 }
 
 // One re-anchoring query (the rows of a lane group; q, i uniform in the group): the exact anchor set within radius
@@ -528,7 +488,7 @@ PCD_DEV void rq_finish(int64_t i, Vec3 q, float r_s, int64_t N, int kstore, floa
 // leaves what `src` covers (StagedSrc: the caller hands the query to the global-memory pass).
 template <int KA, int W, class Src>
 PCD_DEV bool rq_query(const GridView& g, const Src& src, int64_t i, Vec3 q, float r_s, int64_t N, int kstore,
-                      float4* __restrict__ anc, int32_t* __restrict__ alist, int32_t* __restrict__ idx,
+                      float4* __restrict__ anc, float* __restrict__ ak1, int32_t* __restrict__ alist, int32_t* __restrict__ idx,
                       int32_t* __restrict__ spill, unsigned* __restrict__ spill_cnt, unsigned long long* buf,
                       RqCells* wc, const LaneGrp<W>& lg) {
     unsigned long long cap = 0;
@@ -548,31 +508,22 @@ PCD_DEV bool rq_query(const GridView& g, const Src& src, int64_t i, Vec3 q, floa
         if (big) break;
         if (!src.covers(lo, hi)) return false;    // (block-uniform per query: every lane of the group)
         const bool clean = rq_scan_box<KA, W>(g, src, q, lo, hi, cap, buf, cnt, wc, lg);
-#if defined(PCD_EXP_RQ) && PCD_EXP_RQ >= 4      // timing experiment: no finish, no widening (every row spills)
-        if (cnt != -12345) {            // a valid (wrong) list: the row itself; the anchor stays unset
-            if (lg.hl < kstore) idx[lpos(N, i, lg.hl)] = (int32_t)i;
-            if (W + lg.hl < kstore) idx[lpos(N, i, W + lg.hl)] = (int32_t)i;
-            return true;
-        }
-#endif
         ok = clean && cnt > kstore;
         if (ok || !clean) break;
         wave_sync();
     }
-    rq_finish<KA, W>(i, q, r_s, N, kstore, anc, alist, idx, spill, spill_cnt, buf, cnt, cap, ok, big, lg);
+    rq_finish<KA, W>(i, q, r_s, N, kstore, anc, ak1, alist, idx, spill, spill_cnt, buf, cnt, cap, ok, big, lg);
     return true;
 }
 
-// One query per lane group of W lanes (grid-stride): DENSE = every active row (radius from the cell occupancy), else
-// the rows of `list` (the anchor test's failures, radius from the old anchor).  Spilled rows go to `spill` for
-// k_knn_redo_wave.
-#ifndef PCD_RQ_W
-#define PCD_RQ_W 64   // 32 (two queries per wave) measured equal at occupancy 6 and slower at 8 (spills)
-#endif
-template <int KA, bool DENSE, int W = PCD_RQ_W>
+// The steady re-anchoring: one query per wave (grid-stride) over the rows of `list` (the anchor test's failures,
+// radius from the old anchor).  Spilled rows go to `spill` for k_knn_redo_wave.  (Two queries per wave, in 32-lane
+// groups or sharing one scan, measured equal or slower: DESIGN.md §3.)
+template <int KA, int W = 64>
 __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, const float4* __restrict__ pos,
-                                                                 int64_t N, RowMap rm, int kstore, float r_scale,
-                                                                 float4* __restrict__ anc, int32_t* __restrict__ alist,
+                                                                 int64_t N, RowMap rm, int kstore,
+                                                                 float4* __restrict__ anc, float* __restrict__ ak1,
+                                                                 int32_t* __restrict__ alist,
                                                                  int32_t* __restrict__ idx,
                                                                  const int32_t* __restrict__ list,
                                                                  const unsigned* __restrict__ list_cnt,
@@ -586,35 +537,26 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
     const LaneGrp<W> lg(lane);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int gid = wv * G + lane / W;           // group in the block
-    const int64_t cnt_rows = DENSE ? rm.nq : (int64_t)*list_cnt;
+    (void)rm;
+    const int64_t cnt_rows = (int64_t)*list_cnt;
     const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
     unsigned long long* buf = s_buf[gid];
     for (int64_t t0 = lb * 4 * G + gid; t0 < cnt_rows; t0 += (int64_t)gridDim.x * 4 * G) {
-        int64_t i = DENSE ? rm(t0) : (int64_t)list[t0];
+        int64_t i = (int64_t)list[t0];
         if (W == 64) i = (int64_t)rfl((uint32_t)i);
         const float4 p4 = pos[i];
         const Vec3 q = v3(p4.x, p4.y, p4.z);
-        // The search radius r: DENSE from the occupancy of the query's cell, else from the old anchor's D (the local
-        // KA-th distance; the cap (D + |q - a|)^2 that bounds the KA-th key at q is ~2x the area to scan).  The new
-        // anchor set is the KA nearest within r, or -- when fewer than KA points lie within r -- ALL of them, with
-        // D = r: every other snapshot point is then farther than r, which is all the anchor test needs.
-        float r_s;
-        if (DENSE) {
-            const int cx = min(max(cell_coord(q.x, g.ox, g.inv_h), 0), g.dx - 1);
-            const int cy = min(max(cell_coord(q.y, g.oy, g.inv_h), 0), g.dy - 1);
-            const int cz = min(max(cell_coord(q.z, g.oz, g.inv_h), 0), g.dz - 1);
-            uint32_t s = 0, e = 0;
-            const int n = cell_range(g, cx, cy, cz, s, e) ? (int)(e - s) : 1;
-            r_s = r_scale * g.h * cbrtf(16.f / (float)n);
-        } else {
-            const float4 a = anc[i];
-            if (!(a.w > 0.f)) {                       // no anchor: the wave search grows its own box
-                if (lg.hl == 0) spill[atomicAdd(spill_cnt, 1u)] = (int32_t)i;
-                continue;
-            }
-            r_s = a.w * PCD_RQ_RSCALE;
+        // The search radius r from the old anchor's D (the local KA-th distance; the cap (D + |q - a|)^2 that bounds
+        // the KA-th key at q is ~2x the area to scan).  The new anchor set is the KA nearest within r, or -- when
+        // fewer than KA points lie within r -- ALL of them, with D = r: every other snapshot point is then farther
+        // than r, which is all the anchor test needs.
+        const float4 a = anc[i];
+        if (!(a.w > 0.f)) {                           // no anchor: the wave search grows its own box
+            if (lg.hl == 0) spill[atomicAdd(spill_cnt, 1u)] = (int32_t)i;
+            continue;
         }
-        const bool done = rq_query<KA, W>(g, GridSrc{&g}, i, q, r_s, N, kstore, anc, alist, idx, spill, spill_cnt, buf,
+        const float r_s = a.w * PCD_RQ_RSCALE;
+        const bool done = rq_query<KA, W>(g, GridSrc{&g}, i, q, r_s, N, kstore, anc, ak1, alist, idx, spill, spill_cnt, buf,
                                           &s_cells[gid], lg);
         (void)done;                                   // (GridSrc covers every box)
         wave_sync();                                  // buf is free for the next query
@@ -734,14 +676,11 @@ PCD_DEV void rq_scan_box_q(const GridView& g, const Src& src, const Vec3 (&q)[Q]
 }
 
 #ifndef PCD_DENSE_Q
-#define PCD_DENSE_Q 2        // queries per wave of the dense first anchoring (0: one, k_knn_requery<KA, true>; A/B at 10M: first iteration 23.6 / 21.8 / 25.4 ms at 0 / 2 / 4)
+#define PCD_DENSE_Q 2        // queries per wave of the dense first anchoring (A/B at 10M: first iteration 23.6 / 21.8 / 25.4 ms at 1 / 2 / 4)
 #endif
 #ifndef PCD_DQ_OCC
 #define PCD_DQ_OCC 6          // A/B at 10M: first iteration 21.7 / 20.7 / 21.3 ms at 4 (5 by VGPRs) / 6 / 7 waves per SIMD
 #endif
-// LIST (steady re-anchoring): the rows of list[0 .. *list_cnt) (the anchor test's failures, in row order, so
-// consecutive entries are spatial neighbours) with the radius of their old anchor, as k_knn_requery<KA, false>; a row
-// without an anchor spills to the wave search.
 // The dense radius of every active row, r_scale h (16 / n)^(1/3) with n the occupancy of the row's cell, one lane a
 // row: the hash probe and the cube root leave the waves of k_knn_dense_q, where every query paid them at full wave
 // width before its box was known (same float arithmetic: the same radius).
@@ -766,16 +705,16 @@ __global__ void k_dense_radius(GridView g, const float4* __restrict__ pos, RowMa
     }
 }
 
-template <int KA, int Q, bool LIST = false>
+// rpre: every active row's radius (k_dense_radius); bpre (optional): its query box, else computed here.
+template <int KA, int Q>
 __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, const float4* __restrict__ pos, int64_t N,
-                                                                RowMap rm, int kstore, float r_scale,
-                                                                float4* __restrict__ anc, int32_t* __restrict__ alist,
-                                                                int32_t* __restrict__ idx, int32_t* __restrict__ spill,
+                                                                RowMap rm, int kstore, float4* __restrict__ anc,
+                                                                float* __restrict__ ak1,
+                                                                int32_t* __restrict__ alist, int32_t* __restrict__ idx,
+                                                                int32_t* __restrict__ spill,
                                                                 unsigned* __restrict__ spill_cnt,
-                                                                const int32_t* __restrict__ list = nullptr,
-                                                                const unsigned* __restrict__ list_cnt = nullptr,
-                                                                const float* __restrict__ rpre = nullptr,
-                                                                const uint4* __restrict__ bpre = nullptr) {
+                                                                const float* __restrict__ rpre,
+                                                                const uint4* __restrict__ bpre) {
     constexpr int W = 64;
     __shared__ unsigned long long s_buf[4][Q][RqSurv<W>::n];
     __shared__ RqCells s_cells[4];
@@ -783,7 +722,7 @@ __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, con
     const LaneGrp<W> lg(lane);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
-    const int64_t nrows = LIST ? (int64_t)*list_cnt : rm.nq;
+    const int64_t nrows = rm.nq;
     for (int64_t t0 = (lb * 4 + wv) * Q; t0 < nrows; t0 += (int64_t)gridDim.x * 4 * Q) {
         int64_t iq[Q];
         Vec3 q[Q];
@@ -798,30 +737,14 @@ __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, con
         for (int j = 0; j < Q; ++j) {
             act[j] = t0 + j < nrows;
             const int64_t tj = act[j] ? t0 + j : t0;
-            iq[j] = (int64_t)rfl((uint32_t)(LIST ? (int64_t)list[tj] : rm(tj)));
+            iq[j] = (int64_t)rfl((uint32_t)rm(tj));
             const float4 p4 = pos[iq[j]];
             q[j] = v3(p4.x, p4.y, p4.z);
-            if constexpr (LIST) {
-                const float4 a = anc[iq[j]];
-                if (!(a.w > 0.f)) {                     // no anchor: the wave search grows its own box
-                    if (act[j] && lg.hl == 0) spill[atomicAdd(spill_cnt, 1u)] = (int32_t)iq[j];
-                    act[j] = false;
-                }
-                rs[j] = a.w > 0.f ? a.w * PCD_RQ_RSCALE : g.h;
-            } else if (rpre) {
-                rs[j] = rpre[tj];                       // (k_dense_radius)
-            } else {
-                const int cx = min(max(cell_coord(q[j].x, g.ox, g.inv_h), 0), g.dx - 1);
-                const int cy = min(max(cell_coord(q[j].y, g.oy, g.inv_h), 0), g.dy - 1);
-                const int cz = min(max(cell_coord(q[j].z, g.oz, g.inv_h), 0), g.dz - 1);
-                uint32_t s = 0, e = 0;
-                const int n = cell_range(g, cx, cy, cz, s, e) ? (int)(e - s) : 1;
-                rs[j] = r_scale * g.h * cbrtf(16.f / (float)n);
-            }
+            rs[j] = rpre[tj];                           // (k_dense_radius)
             cap[j] = ((unsigned long long)__float_as_uint(rs[j] * rs[j]) << 32) | 0xFFFFFFFFull;
             int l3[3], h3[3];
             uint4 bx = make_uint4(0u, 0u, 0u, 1u);
-            if (!LIST && bpre) bx = bpre[tj];          // (k_dense_radius)
+            if (bpre) bx = bpre[tj];                    // (k_dense_radius)
             if (bx.w == 0u) {
                 l3[0] = (int)(bx.x & 0xFFFFu); l3[1] = (int)(bx.x >> 16); l3[2] = (int)(bx.y & 0xFFFFu);
                 h3[0] = (int)(bx.y >> 16); h3[1] = (int)(bx.z & 0xFFFFu); h3[2] = (int)(bx.z >> 16);
@@ -846,13 +769,13 @@ __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, con
         for (int j = 0; j < Q; ++j) {
             if (!act[j]) continue;
             if (clean[j] && cnt[j] > kstore) {
-                rq_finish<KA, W>(iq[j], q[j], rs[j], N, kstore, anc, alist, idx, spill, spill_cnt, bufs[j], cnt[j],
+                rq_finish<KA, W>(iq[j], q[j], rs[j], N, kstore, anc, ak1, alist, idx, spill, spill_cnt, bufs[j], cnt[j],
                                  cap[j], true, false, lg);
             } else {
                 // alone: its own box (an oversized one spills in there), the radius widened when too few were found
                 wave_sync();
                 (void)rq_query<KA, W>(g, GridSrc{&g}, iq[j], q[j], clean[j] ? rs[j] * 1.6f : rs[j], N, kstore, anc,
-                                      alist, idx, spill, spill_cnt, bufs[j], &s_cells[wv], lg);
+                                      ak1, alist, idx, spill, spill_cnt, bufs[j], &s_cells[wv], lg);
             }
             wave_sync();
         }

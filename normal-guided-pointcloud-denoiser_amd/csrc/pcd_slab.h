@@ -376,7 +376,7 @@ int pcd_slab_iterate(pcd_denoiser* dn, pcd_comm* c, const pcd_denoise_params* p,
     const Band band = overlap ? Band{dn->own, dn->bflag} : kNoBand;
     // the fused loop's copy-free Gauss-Seidel phases (pcd_denoiser_iterate's condition): halo rows receive their
     // positions in both buffers, so a neighbour read through SplitRows sees the current position either way
-    const bool split = PCD_PHASE_SPLIT && !p->jacobi && p->nphases == 3 &&
+    const bool split = !p->jacobi && p->nphases == 3 &&
                        ((1u << p->phase_class[0]) | (1u << p->phase_class[1]) | (1u << p->phase_class[2])) == 7u &&
                        !phase_is_global(p, 1) && !phase_is_global(p, 2);
     for (int it = 0; it < iterations; ++it) {

@@ -20,12 +20,6 @@
 namespace pcd {
 
 static constexpr int kWaveSurv = 256;   // survivor slots per wave (4 per lane)
-#ifdef PCD_WKNN_STATS   // experiment builds only: queries, chunks, candidate rows, reduces, final survivors, sorts>128
-__device__ unsigned long long g_wstats[8];
-#define PCD_WSTAT(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_wstats[i], (unsigned long long)(v)); } while (0)
-#else
-#define PCD_WSTAT(i, v) ((void)0)
-#endif
 
 PCD_DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -182,8 +176,6 @@ PCD_DEV void wave_scan_chunk(const GridView& g, Vec3 q, const uint2 (&cr)[kCells
     }
     const uint32_t incl = lane_scan_incl<64>(run);
     const uint32_t total = (uint32_t)__shfl((int)incl, 63);
-    PCD_WSTAT(1, 1);
-    PCD_WSTAT(2, total);
     if (total == 0) return;
     const uint32_t excl = incl - run;
     wave_sync();                         // the previous chunk's readers are done with wc
@@ -217,7 +209,6 @@ PCD_DEV void wave_scan_chunk(const GridView& g, Vec3 q, const uint2 (&cr)[kCells
             const uint32_t j = j0 + (uint32_t)(u * 64 + lane);
             if (j0 + (uint32_t)(u * 64) < total) {
                 if (cnt > kWaveSurv - 64) {  // make room: keep the K best, tighten the cap
-                    PCD_WSTAT(3, 1);
                     int kept;
                     const unsigned long long top = wave_sort_survivors(buf, cnt, lane, K, kept);
                     const unsigned long long kth_key = __shfl(top, K - 1);
@@ -430,10 +421,6 @@ PCD_DEV unsigned long long wave_knn(const GridView& g, Vec3 q, unsigned long lon
     const float r = sqrtf(__uint_as_float((unsigned)(cap >> 32))) * 1.0001f + 1e-30f;
     cell_box(g, q, r, lo, hi);
     wave_scan_box<K>(g, q, lo, hi, cap, buf, cnt, wc, lane);
-    PCD_WSTAT(0, 1);
-    PCD_WSTAT(4, cnt);
-    PCD_WSTAT(5, cnt > 128);
-    PCD_WSTAT(6, (hi[0] - lo[0] + 1) * (hi[1] - lo[1] + 1) * (hi[2] - lo[2] + 1));
     int kept;
     return wave_sort_survivors(buf, cnt, lane, 0, kept);
 }

@@ -41,6 +41,36 @@ import pcd_native as nat
 
 
 # ----------------------------------------------------------------------------------------------- partition
+def _cut(snap: torch.Tensor, world: int, axis: int | None = None, weights: torch.Tensor | None = None):
+    """The slab cut of `snap` (every rank computes the same one): (axis, axis key, owner rank of each point, per-rank
+    lo / hi of the owned keys).  Equal point counts along the longest bbox axis, or (weights, [N] >= 0) equal shares of
+    the cumulative weight; each rank owns at least one point; ties on the axis broken by index (stable sort)."""
+    n = snap.size(0)
+    assert world >= 1 and n >= world, "need at least one point per rank"
+    if axis is None:
+        axis = int(torch.argmax(snap.max(0).values - snap.min(0).values).item())
+    key = snap[:, axis].contiguous()
+    order = torch.sort(key, stable=True).indices
+    if weights is None:
+        bounds = [(r * n) // world for r in range(world + 1)]
+    else:
+        cw = torch.cumsum(weights.to(snap.device, torch.float64)[order], 0)
+        tot = float(cw[-1])
+        cuts = torch.tensor([tot * r / world for r in range(1, world)], dtype=torch.float64, device=snap.device)
+        inner = torch.searchsorted(cw, cuts).tolist() if world > 1 else []
+        bounds = [0] + [int(b) for b in inner] + [n]
+        for r in range(1, world + 1):                           # at least one point per rank, monotone
+            bounds[r] = min(max(bounds[r], bounds[r - 1] + 1), n - (world - r))
+    owner = torch.empty(n, dtype=torch.int64, device=snap.device)
+    lo, hi = [], []
+    for r in range(world):
+        owner[order[bounds[r]:bounds[r + 1]]] = r
+        ks = key[order[bounds[r]:bounds[r + 1]]]
+        lo.append(float(ks[0]))
+        hi.append(float(ks[-1]))
+    return axis, key, owner, lo, hi
+
+
 @dataclass
 class Spheres:
     """Coverage spheres of the sparse points near a cut (cut_spheres): centre ids (global), radii, and the snapshot
@@ -85,31 +115,8 @@ class SlabPlan:
         axis instead of equal point counts (each rank still owns at least one point).  spheres (optional): every
         member of a sphere is local to the owner of its centre, beyond the band."""
         snap = snap.detach()
-        n = snap.size(0)
-        assert world >= 1 and n >= world, "need at least one point per rank"
-        ext = snap.max(0).values - snap.min(0).values
-        if axis is None:
-            axis = int(torch.argmax(ext).item())
-        key = snap[:, axis].contiguous()
-        order = torch.sort(key, stable=True).indices           # ties by index: deterministic on every rank
-        owner = torch.empty(n, dtype=torch.int64, device=snap.device)
-        if weights is None:
-            bounds = [(r * n) // world for r in range(world + 1)]
-        else:
-            cw = torch.cumsum(weights.to(snap.device, torch.float64)[order], 0)
-            tot = float(cw[-1])
-            cuts = torch.tensor([tot * r / world for r in range(1, world)], dtype=torch.float64, device=snap.device)
-            inner = torch.searchsorted(cw, cuts).tolist() if world > 1 else []
-            bounds = [0] + [int(b) for b in inner] + [n]
-            for r in range(1, world + 1):                       # at least one point per rank, monotone
-                bounds[r] = min(max(bounds[r], bounds[r - 1] + 1), n - (world - r))
-        lo, hi, local = [], [], []
-        for r in range(world):
-            owner[order[bounds[r]:bounds[r + 1]]] = r
-        for r in range(world):
-            ks = key[order[bounds[r]:bounds[r + 1]]]
-            lo.append(float(ks[0]))
-            hi.append(float(ks[-1]))
+        axis, key, owner, lo, hi = _cut(snap, world, axis, weights)
+        local = []
         for r in range(world):
             inside = (key >= lo[r] - halo) & (key <= hi[r] + halo)
             if spheres is not None and spheres.ids.numel():
@@ -302,6 +309,9 @@ class HipSlabEngine:
     def status(self) -> int:
         return self.fused.status()
 
+    def coverage_excess(self) -> tuple:
+        return self.fused.coverage_excess()
+
     # the one-call iteration (pcd_slab_iterate)
     native = True
 
@@ -440,14 +450,21 @@ class SlabDenoiser:
         self.comm = self.t.native_comm() if self.native else None
         self.check_every, self.halo_growth, self.max_replans = int(check_every), float(halo_growth), int(max_replans)
         self.replans = 0
+        self.replan_log = []       # per re-plan: why (coverage: what failed and by how much / rebalance) and the new halo
         self.e = None
+        # the default halo (halo=None, HIP engine, world > 1) is the band + coverage spheres of cut_spheres, recomputed
+        # for every new cut (rebalance); a coverage failure grows only the component that failed, by what it lacked
+        self._auto_halo = halo is None and world > 1 and engine_factory is None
+        self._sphere_quantile = float(sphere_quantile)
+        self._band_floor = 0.0     # the band a coverage failure grew to (a re-cut never goes below it)
+        self._sphere_scale = 1.0   # the spheres' growth by coverage failures
         if rank == 0:
             self.snap_pos, self.snap_n = snap_pos.detach().contiguous(), snap_n.detach().contiguous()
             self.dev = self.snap_pos.device
             self._spheres = None
             if halo is None:
                 if world > 1:
-                    halo, sid, srad = cut_spheres(self.snap_pos, world, k_max, quantile=sphere_quantile)
+                    halo, sid, srad = cut_spheres(self.snap_pos, world, k_max, quantile=sphere_quantile, weights=weights)
                     self._spheres = Spheres.around(self.snap_pos, sid, srad) if engine_factory is None else None
                 else:
                     halo = 0.0
@@ -590,19 +607,27 @@ class SlabDenoiser:
         g = self._gather_to0(torch.cat([owned_pos, owned_n], 1))
         return None if g is None else (g[:, :3], g[:, 3:])
 
-    def _replan(self, halo=None, weights=None, state="now"):
+    def _replan(self, halo=None, weights=None, state="now", sphere_scale=None):
         """Re-cut every rank from the frozen snapshot, taking over `state` (global current pos, n on the
-        coordinator, None on the other ranks; "now": gather the present iterate).  Collective: all ranks call it
-        together."""
+        coordinator, None on the other ranks; "now": gather the present iterate).  halo / sphere_scale (coordinator):
+        the grown band and the factor for the coverage spheres (None: unchanged); weights: a new cost-weighted cut --
+        with the default halo its band and spheres are recomputed for the new faces (the old cut's spheres would
+        miss the sparse points near the moved cuts).  Collective: all ranks call it together."""
         if isinstance(state, str):
             state = self._global_state(*self._owned_state_now())
         plan = None
         if self.t.rank == 0:
-            if halo is not None and self._spheres is not None and self.plan.halo > 0:
-                self._spheres = self._spheres.scaled(self.snap_pos, halo / self.plan.halo)   # (widened alike)
-            halo = self.plan.halo if halo is None else halo
             if weights is not None:
                 self._weights = weights
+            if weights is not None and self._auto_halo:
+                band, sid, srad = cut_spheres(self.snap_pos, self.t.world, self.k_max, quantile=self._sphere_quantile,
+                                              axis=self.plan.axis, weights=self._weights)
+                halo = max(band, self._band_floor)
+                self._spheres = Spheres.around(self.snap_pos, sid, srad * self._sphere_scale)
+            else:
+                if sphere_scale is not None and self._spheres is not None:
+                    self._spheres = self._spheres.scaled(self.snap_pos, sphere_scale)
+                halo = self.plan.halo if halo is None else halo
             plan = SlabPlan.build(self.snap_pos, self.t.world, halo, axis=self.plan.axis, weights=self._weights,
                                   spheres=self._spheres)
         self._setup(plan, state)
@@ -619,16 +644,53 @@ class SlabDenoiser:
         self.t.all_reduce(f, "max")
         return bool(f.item())
 
+    def _max_over_ranks(self, vals):
+        """Element-wise max of a few float32 scalars over the ranks (libpcd's communicator on the native path)."""
+        if self.t.world == 1:
+            return list(vals)
+        if self.native:
+            t = torch.tensor(vals, dtype=torch.float32, device=nat.device())
+            self.comm.allreduce_(t, nat.OP_MAX)
+        else:
+            t = torch.tensor(vals, dtype=torch.float32)
+            self.t.all_reduce(t, "max")
+        return [float(x) for x in t.cpu()]
+
+    def _growth(self):
+        """What the failed coverage checks lacked (max over the ranks): the new band and the spheres' factor.  A
+        sphere-less row whose ball left the band box widens the band by 1.5 x its reach past it (at least x 1.1); a
+        sphere row that left its sphere grows every sphere by 1.25 x its ratio; what did not fail stays.  Engines
+        without the diagnostics (the CPU oracle engine) widen both by halo_growth."""
+        bits = self.e.status()
+        have = hasattr(self.e, "coverage_excess")
+        b, s = self.e.coverage_excess() if have else (0.0, 0.0)
+        band_fail, sph_fail = float(bool(bits & 4)), float(bool(bits & 8))
+        band_fail, sph_fail, b, s, have = self._max_over_ranks([band_fail, sph_fail, b, s, 1.0 if have else 0.0])
+        if not have:
+            return self.halo * self.halo_growth, self.halo_growth, {"legacy_growth": self.halo_growth}
+        halo = max(self.halo * 1.1, self.halo + 1.5 * b) if band_fail else self.halo
+        scale = 1.25 * max(s, 1.0) if sph_fail else None
+        return halo, scale, {"band_failed": bool(band_fail), "band_excess": b, "sphere_failed": bool(sph_fail),
+                             "sphere_ratio": s}
+
     def _verify(self):
-        """Coverage check of the iterations since the checkpoint; on a thin halo: restore the checkpoint, widen the
-        halo, re-plan and replay them."""
+        """Coverage check of the iterations since the checkpoint; on a thin halo: restore the checkpoint, grow what
+        failed, re-plan and replay them."""
         while self._any_rank(bool(self.e.status() & 2)):
             if self.replans >= self.max_replans:
                 raise nat.PcdError(f"pcd_slab: halo still too thin after {self.replans} re-plans "
                                    f"(halo {self.halo:.4g})")
+            halo, scale, why = self._growth()
+            self._band_floor = max(self._band_floor, halo)
+            if scale is not None:
+                self._sphere_scale *= scale
             # (the checkpoint is in the order of the plan it was taken under: gathered before the re-cut)
             gstate = self._global_state(*self._ckpt)
-            self._replan(self.halo * self.halo_growth if self.t.rank == 0 else None, state=gstate)
+            before = self.halo
+            self._replan(halo if self.t.rank == 0 else None, state=gstate,
+                         sphere_scale=scale if self.t.rank == 0 else None)
+            self.replan_log.append(dict(why, reason="coverage", halo_before=before, halo_after=self.halo,
+                                        sphere_scale=scale))
             self.replans += 1
             self._ckpt = self._owned_state_now()            # the restored checkpoint, in the new plan's order
             for p in self._pending:
@@ -711,7 +773,9 @@ class SlabDenoiser:
         w_tab = torch.tensor(class_weights, dtype=torch.float32, device=cls.device)
         w_own = w_tab[cls.clamp(0, len(class_weights) - 1)]
         weights = self._gather_to0(w_own[:, None])
+        before = self.halo
         self._replan(weights=None if weights is None else weights[:, 0].to(self.snap_pos.device))
+        self.replan_log.append({"reason": "rebalance", "halo_before": before, "halo_after": self.halo})
         self._since, self._pending, self._ckpt = 0, [], None
 
     def iterate_timed(self, params) -> dict:
@@ -748,13 +812,14 @@ class SlabDenoiser:
 
 
 def cut_spheres(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, quantile: float = 0.999,
-                axis: int | None = None, sphere_margin: float = 1.5):
-    """(band halo, sphere centre ids, sphere radii) for the equal-count cut: the band is `margin` x the `quantile` of
-    the near-face reaches (cut_halo's per-point requirement); every point whose ball reaches farther keeps a
-    sphere of radius sphere_margin x d_k around itself instead (all of its snapshot members local to its owner), so a few
-    sparse points near a cut no longer set every rank's halo (at 80M points on 8 ranks the max-reach halo held ~half
-    as many halo rows as owned ones)."""
-    idx, reach, dk = _cut_reach(snap_pos, world, k, axis)
+                axis: int | None = None, sphere_margin: float = 1.5, weights: torch.Tensor | None = None):
+    """(band halo, sphere centre ids, sphere radii) for the cut SlabPlan.build makes with the same `weights` (None:
+    equal counts): the band is `margin` x the `quantile` of the near-face reaches (cut_halo's per-point requirement);
+    every point whose ball reaches farther keeps a sphere of radius sphere_margin x d_k around itself instead (all of
+    its snapshot members local to its owner), so a few sparse points near a cut no longer set every rank's halo (at
+    80M points on 8 ranks the max-reach halo held ~half as many halo rows as owned ones).  A cost-weighted re-cut
+    moves the faces, so the band and the spheres are recomputed for it (SlabDenoiser._replan)."""
+    idx, reach, dk = _cut_reach(snap_pos, world, k, axis, weights)
     if idx.numel() == 0:
         z = torch.zeros(0, dtype=torch.int64)
         return 0.0, z, torch.zeros(0)
@@ -765,23 +830,14 @@ def cut_spheres(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25
     return band, idx[out], sphere_margin * dk[out]
 
 
-def _cut_reach(snap_pos: torch.Tensor, world: int, k: int, axis: int | None = None):
-    """Per point near a face of the equal-count cut: (global id, reach of its k-ball past its slab's faces, d_k)."""
+def _cut_reach(snap_pos: torch.Tensor, world: int, k: int, axis: int | None = None,
+               weights: torch.Tensor | None = None):
+    """Per point near a face of the cut (_cut with `weights`): (global id, reach of its k-ball past its slab's
+    faces, d_k)."""
     dev = nat.device()
     pos = snap_pos.to(dev)
-    n = pos.size(0)
-    if axis is None:
-        axis = int(torch.argmax(pos.max(0).values - pos.min(0).values))
-    key = pos[:, axis].contiguous()
-    order = torch.sort(key, stable=True).indices
-    bounds = [(r * n) // world for r in range(world + 1)]
-    ks = key[order]
-    lo = [float(ks[bounds[r]]) for r in range(world)]
-    hi = [float(ks[bounds[r + 1] - 1]) for r in range(world)]
+    axis, key, rank_of, lo, hi = _cut(pos, world, axis, None if weights is None else weights.to(dev))
     band = default_halo(pos, k)
-    rank_of = torch.empty(n, dtype=torch.int64, device=dev)
-    for r in range(world):
-        rank_of[order[bounds[r]:bounds[r + 1]]] = r
     lo_t = torch.tensor(lo, device=dev, dtype=key.dtype)[rank_of]
     hi_t = torch.tensor(hi, device=dev, dtype=key.dtype)[rank_of]
     first, last = rank_of == 0, rank_of == world - 1
@@ -798,7 +854,8 @@ def _cut_reach(snap_pos: torch.Tensor, world: int, k: int, axis: int | None = No
     return idx, torch.maximum(up, down), dk
 
 
-def cut_halo(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, axis: int | None = None) -> float:
+def cut_halo(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, axis: int | None = None,
+             weights: torch.Tensor | None = None) -> float:
     """The halo the equal-count cut into `world` slabs needs at the snapshot, times `margin` for the drift of later
     iterations: every snapshot point's k-ball (radius d_k, its k-th neighbour distance) must lie inside its slab
     widened by the halo on the cut axis, so the halo is the largest reach of a ball past its slab's faces,
@@ -808,7 +865,7 @@ def cut_halo(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, a
     later ball that leaves the halo (a re-plan widens it)."""
     if world == 1:
         return 0.0
-    idx, reach, _ = _cut_reach(snap_pos, world, k, axis)
+    idx, reach, _ = _cut_reach(snap_pos, world, k, axis, weights)
     if idx.numel() == 0:
         return 0.0
     return margin * float(reach.max().clamp(min=0))

@@ -283,6 +283,68 @@ def test_rccl_comm_world1_exchange_and_allreduce(gpu):
 
 
 @pytest.mark.gpu
+def test_rccl_comm_world1_sendrecv_self(gpu):
+    """pcd_comm_sendrecv's RCCL branch (the coordinator hand-out and the re-plan gather ride on it): a route to itself
+    through ncclSend / ncclRecv, byte counts that are multiples of 4 but not of 16 (odd row counts of 4-byte
+    words), every dtype the hand-out moves, and the one-sided forms (send only / receive only skip the other half)."""
+    comm = nat.Comm.rccl(1, 0, lambda t: t)
+    assert comm.info() == {"world": 1, "rank": 0, "transport": "rccl"}
+    g = torch.Generator(device=gpu).manual_seed(11)
+    for n, dt in ((1, torch.float32), (1237, torch.float32), (3 * 4001, torch.int32), (999, torch.float64)):
+        src = (torch.rand(n, generator=g, device=gpu) * 1e6).to(dt)
+        dst = torch.full_like(src, -7)
+        comm.sendrecv(0, src, 0, dst)
+        torch.cuda.synchronize()
+        assert torch.equal(dst, src), (n, dt)
+    # empty transfers are a no-op on both sides
+    comm.sendrecv(-1, None, -1, None)
+    comm.destroy()
+
+
+def _sendrecv_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tr = TorchTransport(rccl=False)
+        comm = tr.native_comm()
+        assert comm.info() == {"world": world, "rank": rank, "transport": "host"}
+        # a ring: every rank sends (rank + 1) * 1237 words to its right neighbour and receives its left neighbour's
+        right, left = (rank + 1) % world, (rank - 1) % world
+        send = torch.arange((rank + 1) * 1237, dtype=torch.int32, device=dev) * (rank + 3)
+        recv = torch.full(((left + 1) * 1237,), -1, dtype=torch.int32, device=dev)
+        comm.sendrecv(right, send, left, recv)
+        torch.cuda.synchronize()
+        expect = torch.arange((left + 1) * 1237, dtype=torch.int32, device=dev) * (left + 3)
+        ok = torch.equal(recv, expect)
+        # one-sided: rank 0 only sends, rank 1 only receives (the coordinator hand-out's pattern)
+        if rank == 0:
+            comm.sendrecv(1, torch.full((5,), 2.5, device=dev), -1, None)
+        elif rank == 1:
+            r = torch.zeros(5, device=dev)
+            comm.sendrecv(-1, None, 0, r)
+            torch.cuda.synchronize()
+            ok = ok and bool((r == 2.5).all())
+        np.save(f"{out_path}.{rank}.npy", np.array([ok]))
+        tr.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_host_comm_world2_sendrecv_ring(gpu, tmp_path):
+    """pcd_comm_sendrecv over the host-callback transport between two processes sharing the GPU: a ring exchange of
+    unequal odd-sized int32 buffers, then the one-sided send / receive of the coordinator hand-out."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "sr")
+    mp.spawn(_sendrecv_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    assert all(bool(np.load(f"{out}.{r}.npy")[0]) for r in range(2))
+
+
+@pytest.mark.gpu
 def test_hip_slab_world2_thin_halo_replans_and_matches_one_gpu(gpu, tmp_path):
     """A deliberately thin halo (1/20 of default_halo): the first coverage check fails on both ranks, the driver
     restores its checkpoint, widens the halo and re-plans from the frozen snapshot, replays -- and ends where the

@@ -1,5 +1,5 @@
 """Time the dense first re-anchoring alone (diagnostic, not a test): one K1 stage of a fresh denoiser (every row
-re-anchored by k_knn_requery<64, true>) at 10M points, nothing after it -- safe for timing-experiment builds whose
+re-anchored by k_dense_radius + k_knn_dense_q<64, 2>) at 10M points, nothing after it -- safe for timing-experiment builds whose
 lists are wrong (no later stage gathers through them).  usage: PCD_LIB=... python tools/dense_probe.py [n] [reps]"""
 import os
 import sys

@@ -30,13 +30,6 @@ def main():
         t = fused.timing()
         r = fused.redo_rows()
         extra = ""
-        if hasattr(nat.lib(), "pcd_debug_wstats"):     # experiment build with wave-search counters
-            import ctypes
-            st = (ctypes.c_ulonglong * 8)()
-            nat.lib().pcd_debug_wstats(st, 1)
-            q = max(st[0], 1)
-            extra = (f"  | wave: q {st[0]} chunks/q {st[1] / q:.2f} rows/q {st[2] / q:.0f} reduces/q {st[3] / q:.2f} "
-                     f"surv/q {st[4] / q:.0f} >128 {st[5] / q:.2f} boxcells/q {st[6] / q:.1f}")
         if hasattr(fused, "tile_stats"):
             ts = fused.tile_stats()
             extra += (f"  | spilled to the exact wave search {ts['spilled']} (big box {ts['spilled_big_box']}, "
