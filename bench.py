@@ -84,7 +84,7 @@ def k1_kernels(k, ku, seeding, anchoring):
     c = knn_cap(max(k, ku))
     unit = "true"    # k_nvt1<C, UNIT>: every timed iteration runs on the loop's own unit normals
     if seeding and anchoring and c <= 32:
-        return [f"k_knn_anchor<{c}, {2 * c}>", "k_compact_fail", f"k_knn_requery<{2 * c}, false, 64>",
+        return [f"k_knn_anchor<{c}, {2 * c}>", "k_compact_fail", f"k_knn_requery<{2 * c}, 64>",
                 f"k_knn_redo_wave<{2 * c}, false>", f"k_nvt1<{c}, {unit}>"]
     return [f"k_knn_nvt1<{c}, {'true' if seeding else 'false'}>"]
 

@@ -335,7 +335,7 @@ static constexpr int kAnchorBS = PCD_ANCHOR_BS;
 template <int K, int KA>
 __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridView g, const float4* __restrict__ pos, int64_t N,
                                                           RowMap rm, int kstore, const float4* __restrict__ anc,
-                                                          const float* __restrict__ ak1, const int32_t* __restrict__ alist,
+                                                          const int32_t* __restrict__ alist,
                                                           int32_t* __restrict__ idx, uint8_t* __restrict__ fail) {
     static_assert(KA == 2 * K && KA <= 64, "anchor lists hold twice the list cap; 6 slot bits");
     __shared__ uint32_t s_r[KA * kAnchorBS];
@@ -367,10 +367,6 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
             // every list point is within D of the anchor, hence within D + delta of q
             const float R = (a.w + delta) * (1.f + 1e-5f);
             const float S = 67108864.f / fmaxf(R * R, 1e-30f);
-            // the members that can rank among the first kstore + 1 at q: distance band <= cut (pcd_lists.h); the
-            // others read the +inf sentinel row instead (one line every such lane of the wave shares: an infinite
-            // key, they sort last, below stays exact for the certificate)
-            const uint32_t cut = anchor_cut(ak1[i], delta * (1.f + kAnchorEps), a.w);
             uint32_t c[KA];
             int below = 0;
             // slot t -> snapshot rank rt into the LDS map
@@ -393,9 +389,9 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
                 float4 pj[32];
 #pragma unroll
                 for (int u = 0; u < 32; ++u) {
-                    const uint32_t rt = min(anchor_rank(r[u]), (uint32_t)N);
+                    const uint32_t rt = min(r[u], (uint32_t)N);
                     map_store(32 * h + u, rt);
-                    pj[u] = *at32(g.pts, anchor_band(r[u]) <= cut ? rt : (uint32_t)N);
+                    pj[u] = *at32(g.pts, rt);
                 }
                 between();
 #pragma unroll
@@ -438,10 +434,9 @@ __global__ __launch_bounds__(kAnchorBS, PCD_ANCHOR_OCC) void k_knn_anchor(GridVi
             for (int t = 0; t < KA; ++t) {
                 // an unused slot of a partial anchor set holds N: the snapshot's +inf sentinel row (the min keeps
                 // any entry inside the allocation)
-                const uint32_t rt = min(anchor_rank(r[t]), (uint32_t)N);
+                const uint32_t rt = min(r[t], (uint32_t)N);
                 map_store(t, rt);
-                // unconditional load: every gather in flight (members past the cut read the sentinel row)
-                const float d2 = dist2(vi, *at32(g.pts, anchor_band(r[t]) <= cut ? rt : (uint32_t)N));
+                const float d2 = dist2(vi, *at32(g.pts, rt));   // unconditional load: every gather in flight
                 below += d2 < T ? 1 : 0;
                 // clamp below 2^26 in fp32 (2^26 - 1 rounds UP to 2^26, which would wrap to 0 after the shift);
                 // only the sentinel's infinite distance reaches it
@@ -572,7 +567,7 @@ __global__ __launch_bounds__(kNvtBS, PCD_NVT1_OCC) void k_nvt1(GridView g, const
 #endif
 template <int KA, bool DENSE>
 __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g, const float4* __restrict__ pos, int64_t N, RowMap rm,
-                                                        int kstore, float4* __restrict__ anc, float* __restrict__ ak1,
+                                                        int kstore, float4* __restrict__ anc,
                                                         int32_t* __restrict__ alist, int32_t* __restrict__ idx,
                                                         const int32_t* __restrict__ redo,
                                                         const unsigned* __restrict__ redo_cnt, int* __restrict__ err) {
@@ -591,7 +586,7 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
             const float4 a = anc[i];
             // (D + |q - a|)² bounds the KA-th key at q only for a FULL anchor set (KA points within D of a); a partial
             // set (fewer points within its radius, unused slots = N, the +inf sentinel row) gives no such bound
-            if (a.w >= 0.f && anchor_rank((uint32_t)alist[lpos(N, i, KA - 1)]) < (uint32_t)N) cap = anchor_cap(q, a);
+            if (a.w >= 0.f && (uint32_t)alist[lpos(N, i, KA - 1)] < (uint32_t)N) cap = anchor_cap(q, a);
         }
         const unsigned long long top = wave_knn<KA>(g, q, cap, s_buf[wv], &s_cells[wv], lane);
         // a slot without a finite candidate (non-finite query, fewer than KA points) is never stored as an index:
@@ -602,20 +597,14 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
         const bool all_valid = !__any(lane < KA && !valid);
         if (!all_valid && lane == 0) atomicOr(err, 1);
         if (lane < kstore) idx[lpos(N, i, lane)] = r;   // (whole 32-B sectors, pcd_lists.h)
-        // D: the KA-th distance (every other snapshot point is at least this far from the anchor); ak1: the
-        // (K+1)-th, rounded up (the anchor test's gather cut, pcd_lists.h anchor_entry)
-        const float D = sqrtf(__uint_as_float((unsigned)__shfl((int)(unsigned)(top >> 32), KA - 1)));
-        const float dK = sqrtf(__uint_as_float((unsigned)__shfl((int)(unsigned)(top >> 32), KA / 2)));
         {   // the anchor set in rank order (see k_knn_requery), unused slots last
-            uint32_t v[1] = {lane < KA ? anchor_entry((uint32_t)r, sqrtf(__uint_as_float((unsigned)(top >> 32))), D)
-                                       : 0xFFFFFFFFu};
+            uint32_t v[1] = {lane < KA ? (uint32_t)r : 0xFFFFFFFFu};
             grp_bitonic_sort32<64, 1>(v, lane);
             if (lane < KA) alist[lpos(N, i, lane)] = (int32_t)v[0];
         }
-        if (lane == 0) {
-            anc[i] = make_float4(q.x, q.y, q.z, all_valid ? D : __int_as_float(0x7FC00000));
-            ak1[i] = dK * (1.f + 1e-5f);
-        }
+        // D: the KA-th distance (every other snapshot point is at least this far from the anchor)
+        if (lane == KA - 1)
+            anc[i] = make_float4(q.x, q.y, q.z, all_valid ? sqrtf(__uint_as_float((unsigned)(top >> 32))) : __int_as_float(0x7FC00000));
     }
 }
 
@@ -986,7 +975,6 @@ struct pcd_denoiser {
     bool seeding = true;          // use the stored list as an acceptance cap (pcd_denoiser_set_seeding)
     // anchored kNN (list cap <= 32): anchors + their 2K-lists, the redo list of queries that failed the test
     float4* anc = nullptr;
-    float* ak1 = nullptr;         // per row: the anchor set's (K+1)-th distance, rounded up (the anchor test's gather cut)
     int32_t* alist = nullptr;
     int32_t* redo = nullptr;      // rows that failed the anchor test (redo list)
     int32_t* spill = nullptr;     // rows the re-anchoring search hands to the exact-key wave search
@@ -1081,7 +1069,7 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     const int kstore = std::max(p->k, p->k_update);
     const int KA = 2 * K;
     if (!dn->anc) {
-        if (hipMalloc(&dn->anc, N * sizeof(float4)) != hipSuccess || hipMalloc(&dn->ak1, N * sizeof(float)) != hipSuccess ||
+        if (hipMalloc(&dn->anc, N * sizeof(float4)) != hipSuccess ||
             hipMalloc(&dn->alist, (int64_t)2 * knn_cap(dn->kcap) * N * sizeof(int32_t)) != hipSuccess ||
             hipMalloc(&dn->redo, N * sizeof(int32_t)) != hipSuccess ||
             hipMalloc(&dn->spill, N * sizeof(int32_t)) != hipSuccess || hipMalloc(&dn->fail, N) != hipSuccess ||
@@ -1118,18 +1106,18 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
             uint4* bpre = !rm.rows && dn->nvt1_on ? reinterpret_cast<uint4*>(dn->fn) : nullptr;                        \
             hipLaunchKernelGGL(k_dense_radius, grd, blk, 0, st, gv, P, rm, PCD_RQ_RDENSE, rpre, bpre);                 \
             hipLaunchKernelGGL((k_knn_dense_q<2 * C, PCD_DENSE_Q>), grd_dq, blk, 0, st, gv, P, N, rm, kstore,          \
-                               dn->anc, dn->ak1, dn->alist, dn->idx, dn->spill, spill_cnt, rpre, bpre);                \
+                               dn->anc, dn->alist, dn->idx, dn->spill, spill_cnt, rpre, bpre);                         \
         } else {                                                                                                       \
             hipLaunchKernelGGL((k_knn_anchor<C, 2 * C>), grd_anc, dim3(kAnchorBS), 0, st, gv, P, N, rm, kstore,        \
-                               dn->anc, dn->ak1, dn->alist, dn->idx, dn->fail);                                        \
+                               dn->anc, dn->alist, dn->idx, dn->fail);                                                 \
             hipLaunchKernelGGL(k_compact_fail, grd_cmp, dim3(kCompactBS), 0, st, dn->fail, rm, dn->redo, redo_cnt);    \
             if (ev) PCD_HIP(hipEventRecord(ev[1], st));                                                                \
-            hipLaunchKernelGGL((k_knn_requery<2 * C>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, dn->anc, dn->ak1,     \
+            hipLaunchKernelGGL((k_knn_requery<2 * C>), grd_rq, blk, 0, st, gv, P, N, rm, kstore, dn->anc,              \
                                dn->alist, dn->idx, dn->redo, redo_cnt, dn->spill, spill_cnt);                          \
         }                                                                                                              \
         if (ev) PCD_HIP(hipEventRecord(ev[2], st));                                                                    \
         hipLaunchKernelGGL((k_knn_redo_wave<2 * C, false>), grd_wave, blk, 0, st, gv, P, N, rm, kstore, dn->anc,       \
-                           dn->ak1, dn->alist, dn->idx, dn->spill, spill_cnt, dn->err);                                \
+                           dn->alist, dn->idx, dn->spill, spill_cnt, dn->err);                                         \
         if (ev) PCD_HIP(hipEventRecord(ev[3], st));                                                                    \
         if (before_nvt1) PCD_HIP(hipStreamWaitEvent(st, before_nvt1, 0));                                              \
         if (!dn->nvt1_on) {                                                                                            \
@@ -1353,7 +1341,7 @@ int pcd_denoiser_destroy(pcd_denoiser* dn) {
     (void)hipFree(dn->xrad);
     (void)hipFree(dn->edge); (void)hipFree(dn->orig); (void)hipFree(dn->idx); (void)hipFree(dn->cls); (void)hipFree(dn->part);
     (void)hipFree(dn->red); (void)hipFree(dn->gscal); (void)hipFree(dn->err);
-    (void)hipFree(dn->anc); (void)hipFree(dn->ak1); (void)hipFree(dn->alist); (void)hipFree(dn->redo); (void)hipFree(dn->spill);
+    (void)hipFree(dn->anc); (void)hipFree(dn->alist); (void)hipFree(dn->redo); (void)hipFree(dn->spill);
     (void)hipFree(dn->rqs); (void)hipFree(dn->fail); (void)hipFree(dn->probe);
     for (auto e : dn->ev) (void)hipEventDestroy(e);
     delete dn;

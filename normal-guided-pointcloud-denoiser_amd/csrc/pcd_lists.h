@@ -31,24 +31,6 @@ PCD_DEV v4i* lblock(int32_t* base, int64_t N, int64_t i, int g) {
 // Element (i, t).
 PCD_DEV int64_t lpos(int64_t N, int64_t i, int t) { return ((int64_t)(t >> 3) * N + i) * 8 + (t & 7); }
 
-// Anchor-set entries (alist): the snapshot rank in the high 27 bits (N < 2^27) and the member's distance BAND from the
-// anchor in the low 5: b = floor(64 d / D - 32), rounded down and clamped to [0, 31], so that d >= (b + 32) D / 64 for
-// b >= 1 (band 0 holds every member nearer than 33 D / 64).  Entries sort by rank.  The anchor test gathers a member
-// only when its band's lower bound lies under ak1 + 2|q - a| (ak1: the anchor set's (K+1)-th distance, bounded above):
-// a member beyond is farther from q than the first K + 1 members are, so it cannot rank among the first kstore + 1
-// at q (kstore <= K) -- the certified list is the same, with ~40 of the 64 gathers.
-PCD_DEV uint32_t anchor_entry(uint32_t rank, float d, float D) {
-    const float x = fminf(fmaxf((64.f * d / D - 32.f) * (1.f - 1e-5f), 0.f), 31.f);
-    return (rank << 5) | (uint32_t)x;
-}
-PCD_DEV uint32_t anchor_rank(uint32_t e) { return e >> 5; }
-PCD_DEV uint32_t anchor_band(uint32_t e) { return e & 31u; }
-// the largest band the anchor test must gather at delta = |q - a| (NaN inputs: band 0 only)
-PCD_DEV uint32_t anchor_cut(float ak1, float delta, float D) {
-    const float X = (ak1 + 2.f * delta) * (1.f + 1e-5f);
-    return (uint32_t)fminf(fmaxf(64.f * X / D - 32.f + 0.01f, 0.f), 31.f);
-}
-
 // The first ceil(cnt / 8) blocks of row i into l[0 .. K) (K a multiple of 8); entries of blocks past cnt are left
 // untouched.  NT: streamed past L2 (a list read once per pass).
 template <int K, bool NT = false>

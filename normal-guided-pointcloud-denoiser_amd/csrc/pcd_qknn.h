@@ -413,12 +413,11 @@ struct RqStats { unsigned redo_cnt, spill_cnt, spill_big, spill_amb; };
 #define PCD_RQ_OCC 8
 #endif
 // The end of a re-anchoring query once its survivors are in buf[0..cnt) under cap: the exact order checks, then the
-// stored list, the anchor set (rank order, each entry packed with its distance band, pcd_lists.h anchor_entry), its
-// (K+1)-th distance bound ak1 and the anchor -- or the spill list when a check fails (ok = false on entry: the scan
-// was ambiguous or found too few points).
+// stored list, the anchor set (rank order) and the anchor -- or the spill list when a check fails (ok = false on
+// entry: the scan was ambiguous or found too few points).
 template <int KA, int W>
 PCD_DEV void rq_finish(int64_t i, Vec3 q, float r_s, int64_t N, int kstore, float4* __restrict__ anc,
-                       float* __restrict__ ak1, int32_t* __restrict__ alist, int32_t* __restrict__ idx, int32_t* __restrict__ spill,
+                       int32_t* __restrict__ alist, int32_t* __restrict__ idx, int32_t* __restrict__ spill,
                        unsigned* __restrict__ spill_cnt, unsigned long long* buf, int cnt, unsigned long long cap,
                        bool ok, bool big, const LaneGrp<W>& lg) {
     const bool partial = cnt < KA;               // (after a buffer cut cnt == KA)
@@ -452,34 +451,23 @@ PCD_DEV void rq_finish(int64_t i, Vec3 q, float r_s, int64_t N, int kstore, floa
     // whole 32-B sectors of the blocked list layout (pcd_lists.h): lanes 8b .. 8b+7 fill block b of row i
     if (e0 < kstore) idx[lpos(N, i, e0)] = r0;
     if (e1 < kstore) idx[lpos(N, i, e1)] = r1;
-    // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
-    // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))
-    const unsigned long long mx = grp_max_u64<W>(m0 > m1 ? m0 : m1);
-    const float D = partial ? r_s * (1.f - 1e-6f) : sqrtf(__uint_as_float((unsigned)(mx >> 32)));
-    // ak1: an upper bound of the (K+1)-th distance from the anchor (element K of the order; D when the set holds
-    // fewer): the anchor test gathers only the members whose distance band lies under ak1 + 2|q - a|
-    constexpr int K = KA / 2;
-    const uint32_t oK = o.at(K);                     // (a shuffle: every lane of the group executes it)
     // the anchor set is stored in RANK order (unused slots last): the anchor test ranks it by distance itself,
     // and neighbouring rows -- neighbouring lanes of its waves -- then gather nearly the same snapshot rows in the
     // same slot, i.e. the same cache lines, instead of 64 unrelated ones per gather instruction
     {
         constexpr int M = KA > W ? 2 : 1;
         uint32_t v[M];
-        const uint32_t sent = anchor_entry((uint32_t)N, 3.0e38f, D);   // unused slot: the +inf sentinel row
-        v[0] = e0 < KA ? (h0 ? anchor_entry((uint32_t)r0, sqrtf(__uint_as_float((unsigned)(m0 >> 32))), D) : sent)
-                       : 0xFFFFFFFFu;
-        if (M > 1)
-            v[M - 1] = e1 < KA ? (h1 ? anchor_entry((uint32_t)r1, sqrtf(__uint_as_float((unsigned)(m1 >> 32))), D) : sent)
-                               : 0xFFFFFFFFu;
-        grp_bitonic_sort32<W, M>(v, lg.hl);        // (by rank: the rank is the entry's high bits)
+        v[0] = e0 < KA ? (uint32_t)r0 : 0xFFFFFFFFu;
+        if (M > 1) v[M - 1] = e1 < KA ? (uint32_t)r1 : 0xFFFFFFFFu;
+        grp_bitonic_sort32<W, M>(v, lg.hl);
         if (e0 < KA) alist[lpos(N, i, e0)] = (int32_t)v[0];
         if (M > 1 && e1 < KA) alist[lpos(N, i, e1)] = (int32_t)v[M - 1];
     }
-    if (lg.hl == 0) {
-        anc[i] = make_float4(q.x, q.y, q.z, D);
-        ak1[i] = K < cnt ? sqrtf(__uint_as_float((unsigned)(buf[oK & 255u] >> 32))) * (1.f + 1e-5f) : D;
-    }
+    // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
+    // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))
+    const unsigned long long mx = grp_max_u64<W>(m0 > m1 ? m0 : m1);
+    const float D = partial ? r_s * (1.f - 1e-6f) : sqrtf(__uint_as_float((unsigned)(mx >> 32)));
+    if (lg.hl == 0) anc[i] = make_float4(q.x, q.y, q.z, D);
 }
 
 // One re-anchoring query (the rows of a lane group; q, i uniform in the group): the exact anchor set within radius
@@ -488,7 +476,7 @@ PCD_DEV void rq_finish(int64_t i, Vec3 q, float r_s, int64_t N, int kstore, floa
 // leaves what `src` covers (StagedSrc: the caller hands the query to the global-memory pass).
 template <int KA, int W, class Src>
 PCD_DEV bool rq_query(const GridView& g, const Src& src, int64_t i, Vec3 q, float r_s, int64_t N, int kstore,
-                      float4* __restrict__ anc, float* __restrict__ ak1, int32_t* __restrict__ alist, int32_t* __restrict__ idx,
+                      float4* __restrict__ anc, int32_t* __restrict__ alist, int32_t* __restrict__ idx,
                       int32_t* __restrict__ spill, unsigned* __restrict__ spill_cnt, unsigned long long* buf,
                       RqCells* wc, const LaneGrp<W>& lg) {
     unsigned long long cap = 0;
@@ -512,7 +500,7 @@ PCD_DEV bool rq_query(const GridView& g, const Src& src, int64_t i, Vec3 q, floa
         if (ok || !clean) break;
         wave_sync();
     }
-    rq_finish<KA, W>(i, q, r_s, N, kstore, anc, ak1, alist, idx, spill, spill_cnt, buf, cnt, cap, ok, big, lg);
+    rq_finish<KA, W>(i, q, r_s, N, kstore, anc, alist, idx, spill, spill_cnt, buf, cnt, cap, ok, big, lg);
     return true;
 }
 
@@ -522,8 +510,7 @@ PCD_DEV bool rq_query(const GridView& g, const Src& src, int64_t i, Vec3 q, floa
 template <int KA, int W = 64>
 __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, const float4* __restrict__ pos,
                                                                  int64_t N, RowMap rm, int kstore,
-                                                                 float4* __restrict__ anc, float* __restrict__ ak1,
-                                                                 int32_t* __restrict__ alist,
+                                                                 float4* __restrict__ anc, int32_t* __restrict__ alist,
                                                                  int32_t* __restrict__ idx,
                                                                  const int32_t* __restrict__ list,
                                                                  const unsigned* __restrict__ list_cnt,
@@ -556,7 +543,7 @@ __global__ __launch_bounds__(256, PCD_RQ_OCC) void k_knn_requery(GridView g, con
             continue;
         }
         const float r_s = a.w * PCD_RQ_RSCALE;
-        const bool done = rq_query<KA, W>(g, GridSrc{&g}, i, q, r_s, N, kstore, anc, ak1, alist, idx, spill, spill_cnt, buf,
+        const bool done = rq_query<KA, W>(g, GridSrc{&g}, i, q, r_s, N, kstore, anc, alist, idx, spill, spill_cnt, buf,
                                           &s_cells[gid], lg);
         (void)done;                                   // (GridSrc covers every box)
         wave_sync();                                  // buf is free for the next query
@@ -709,7 +696,6 @@ __global__ void k_dense_radius(GridView g, const float4* __restrict__ pos, RowMa
 template <int KA, int Q>
 __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, const float4* __restrict__ pos, int64_t N,
                                                                 RowMap rm, int kstore, float4* __restrict__ anc,
-                                                                float* __restrict__ ak1,
                                                                 int32_t* __restrict__ alist, int32_t* __restrict__ idx,
                                                                 int32_t* __restrict__ spill,
                                                                 unsigned* __restrict__ spill_cnt,
@@ -769,13 +755,13 @@ __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, con
         for (int j = 0; j < Q; ++j) {
             if (!act[j]) continue;
             if (clean[j] && cnt[j] > kstore) {
-                rq_finish<KA, W>(iq[j], q[j], rs[j], N, kstore, anc, ak1, alist, idx, spill, spill_cnt, bufs[j], cnt[j],
+                rq_finish<KA, W>(iq[j], q[j], rs[j], N, kstore, anc, alist, idx, spill, spill_cnt, bufs[j], cnt[j],
                                  cap[j], true, false, lg);
             } else {
                 // alone: its own box (an oversized one spills in there), the radius widened when too few were found
                 wave_sync();
                 (void)rq_query<KA, W>(g, GridSrc{&g}, iq[j], q[j], clean[j] ? rs[j] * 1.6f : rs[j], N, kstore, anc,
-                                      ak1, alist, idx, spill, spill_cnt, bufs[j], &s_cells[wv], lg);
+                                      alist, idx, spill, spill_cnt, bufs[j], &s_cells[wv], lg);
             }
             wave_sync();
         }

@@ -59,7 +59,7 @@ def main():
     # bytes of one seeded iteration: every per-iteration kernel's average bytes x its launches, over the number of
     # iterations (= NVT2 launches); one-time kernels (grid build, load/store, the dense first re-anchoring) excluded
     one_time = ("k_bbox", "k_sample", "k_keys", "k_gather_sorted", "k_count_starts", "k_brick_flags", "k_insert",
-                "k_load", "k_store", "k_edge_len", "k_knn<", "k_nn1", "k_radius")
+                "k_load", "k_store", "k_edge_len", "k_knn<", "k_nn1", "k_radius", "k_dense_radius", "k_knn_dense_q")
     dense = re.compile(r"k_knn_(redo_wave|requery|nvt1)<\d+, true")   # the dense first re-anchoring / unseeded K1
     n_iter = sum(e["launches_fetch"] for kn, v in kernels.items() if kn.startswith("k_nvt2<32") for e in v) or None
     per_iter = None
