@@ -115,14 +115,19 @@ class Pointcloud:
 
 def sample_surface(v: torch.Tensor, f: torch.Tensor, num: int, generator: torch.Generator = None,
                    return_faces: bool = False):
-    """Area-weighted barycentric sampling (the SamplePoints transform's algorithm) -> (pos, face normals[, face ids])."""
+    """Area-weighted barycentric sampling (the SamplePoints transform's algorithm) -> (pos, face normals[, face ids]).
+    Faces are drawn by inversion of the area CDF (float64, scanned on the host) with uniform draws from `generator`:
+    the same distribution as SamplePoints' torch.multinomial, but the same seed gives the same cloud on every call and
+    device (a device multinomial is not bitwise reproducible between calls, so two processes drawing the bench's
+    cloud would hold different clouds)."""
     a, b, c = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
     cr = torch.cross(b - a, c - a, dim=1)
     area = cr.norm(dim=1)
     fn = cr / area.clamp(min=1e-30)[:, None]
     dev = generator.device if generator is not None else v.device
-    prob = (area / area.sum()).to(dev)
-    fid = torch.multinomial(prob, num, replacement=True, generator=generator).to(v.device)
+    cdf = torch.cumsum(area.double().cpu(), 0)
+    u = torch.rand(num, generator=generator, device=dev, dtype=torch.float64) * cdf[-1].item()
+    fid = torch.searchsorted(cdf.to(dev), u).clamp_(max=len(cdf) - 1).to(v.device)
     uv = torch.rand((num, 2), generator=generator, device=dev).to(v.device)
     flip = uv.sum(1) > 1
     uv[flip] = 1 - uv[flip]

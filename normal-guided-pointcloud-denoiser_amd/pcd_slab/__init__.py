@@ -691,6 +691,10 @@ class SlabDenoiser:
                          sphere_scale=scale if self.t.rank == 0 else None)
             self.replan_log.append(dict(why, reason="coverage", halo_before=before, halo_after=self.halo,
                                         sphere_scale=scale))
+            if self.t.rank == 0:
+                import sys
+                print(f"pcd_slab: coverage re-plan {self.replans + 1}: {self.replan_log[-1]}", file=sys.stderr,
+                      flush=True)
             self.replans += 1
             self._ckpt = self._owned_state_now()            # the restored checkpoint, in the new plan's order
             for p in self._pending:
@@ -831,9 +835,12 @@ def cut_spheres(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25
 
 
 def _cut_reach(snap_pos: torch.Tensor, world: int, k: int, axis: int | None = None,
-               weights: torch.Tensor | None = None):
-    """Per point near a face of the cut (_cut with `weights`): (global id, reach of its k-ball past its slab's
-    faces, d_k)."""
+               weights: torch.Tensor | None = None, chunk: int = 8_000_000):
+    """Per point near a face of the cut (_cut with `weights`): (global id, reach of its k-ball past its slab's faces,
+    d_k).  'Near' = within default_halo of a face (the sampled bound, the quantile's population) OR any point whose
+    own k-ball crosses a face: d_k comes from every point (in chunks), so a sparse outlier far from a face with a
+    ball past it -- which a sampled bound misses -- is priced too (round 6: the 80M / 8-rank rehearsal's first
+    iteration failed its coverage check on such points)."""
     dev = nat.device()
     pos = snap_pos.to(dev)
     axis, key, rank_of, lo, hi = _cut(pos, world, axis, None if weights is None else weights.to(dev))
@@ -841,17 +848,19 @@ def _cut_reach(snap_pos: torch.Tensor, world: int, k: int, axis: int | None = No
     lo_t = torch.tensor(lo, device=dev, dtype=key.dtype)[rank_of]
     hi_t = torch.tensor(hi, device=dev, dtype=key.dtype)[rank_of]
     first, last = rank_of == 0, rank_of == world - 1
-    near = ((key > hi_t - band) & ~last) | ((key < lo_t + band) & ~first)
-    idx = torch.nonzero(near).flatten()
-    if idx.numel() == 0:
-        return idx, torch.zeros(0, device=dev), torch.zeros(0, device=dev)
     g = nat.Grid(pos, k_hint=k)
-    _, d2 = g.knn(pos[idx].contiguous(), k, with_d2=True)
-    dk = d2[:, -1].sqrt()
-    q = key[idx]
-    up = torch.where(last[idx], torch.zeros_like(dk), q + dk - hi_t[idx])
-    down = torch.where(first[idx], torch.zeros_like(dk), lo_t[idx] - q + dk)
-    return idx, torch.maximum(up, down), dk
+    n = pos.size(0)
+    dk = torch.empty(n, dtype=torch.float32, device=dev)
+    for c0 in range(0, n, chunk):
+        _, d2 = g.knn(pos[c0:c0 + chunk].contiguous(), k, with_d2=True, idx_bits=32)
+        dk[c0:c0 + chunk] = d2[:, -1].sqrt()
+        del d2
+    up = torch.where(last, torch.zeros_like(dk), key + dk - hi_t)
+    down = torch.where(first, torch.zeros_like(dk), lo_t - key + dk)
+    reach = torch.maximum(up, down)
+    near = ((key > hi_t - band) & ~last) | ((key < lo_t + band) & ~first) | (reach > 0)
+    idx = torch.nonzero(near).flatten()
+    return idx, reach[idx], dk[idx]
 
 
 def cut_halo(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, axis: int | None = None,

@@ -141,3 +141,29 @@ class CpuMeshEngine:
 
     def sweep(self):
         self.v = torch.from_numpy(O.mesh_update(self.v.numpy(), self.f, self.fn, k=1))
+
+
+class CpuSlabEngineDiag(CpuSlabEngine):
+    """The oracle engine with libpcd's coverage diagnostics (pcd_denoiser_coverage_excess, sphere-less rows only):
+    a failed check sets bits 2 and 4 and records the farthest reach of a k-ball past the coverage box, so the driver
+    grows the band by what it lacked instead of by halo_growth."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.excess = 0.0
+
+    def stage(self, params, stage, phase=0, red=None):
+        if stage == nat.STAGE_KNN_NVT1:
+            kstore = max(params.k, params.k_update)
+            a = self.active
+            _, dist = self.knn.query(self.pos[a], kstore)
+            r = dist[:, -1] * (1 + 1e-6)
+            q = self.pos[a].astype(np.float64)
+            ex = np.maximum(self.lo - (q - r[:, None]), (q + r[:, None]) - self.hi).max() if len(a) else 0.0
+            if ex > 0:
+                self.err |= 2 | 4
+                self.excess = max(self.excess, float(ex))
+        super().stage(params, stage, phase, red)
+
+    def coverage_excess(self):
+        return (self.excess if self.err & 4 else 0.0), 0.0

@@ -107,10 +107,8 @@ def test_sample_obj_on_device(gpu, tmp_path):
         expect = float(area[chunk].sum() / area.sum() * n)
         got = float(counts[chunk].sum())
         assert abs(got - expect) < 5 * math.sqrt(expect) + 1, (got, expect)
-    # sampleObj is this very call (device multinomial draws are not bitwise reproducible between calls, so the
-    # two sample sets are compared as distributions: centroid within 5 standard errors, unit normals)
-    se = pos2.double().std(0) / n ** 0.5
-    assert ((pc.v.double().mean(0) - pos2.double().mean(0)).abs() < 5 * se * 2 ** 0.5).all()
+    # sampleObj is this very call, and the inverse-CDF draws reproduce bit for bit (on the host too)
+    assert torch.equal(pc.v, pos2) and torch.equal(pc.n, nrm2)
     assert torch.allclose(pc.n.norm(dim=1), torch.ones(1, device=gpu), atol=1e-5)
 
 
@@ -119,6 +117,9 @@ def test_bench_cloud_is_drawn_on_device(gpu):
     from bench import make_cloud
     pos, nrm, diag, surf = make_cloud(2_000_000, 2, gpu, clean=True)
     assert pos.device.type == "cuda" and surf.device.type == "cuda"
+    # the same seed draws the same cloud again (every rank of a slab run and every bench process hold one cloud)
+    pos2, nrm2, _ = make_cloud(2_000_000, 2, gpu)
+    assert torch.equal(pos, pos2) and torch.equal(nrm, nrm2)
     off = (pos - surf).double()
     assert torch.allclose(off.std(0), torch.full((3,), 0.005 * diag, dtype=torch.float64, device=gpu), rtol=0.01)
     assert torch.allclose(nrm.norm(dim=1), torch.ones(1, device=gpu), atol=1e-5)

@@ -135,12 +135,8 @@ def test_sample_obj_area_weighted(tmp_path):
     pc = Pointcloud.sampleObj(str(p), n, generator=torch.Generator().manual_seed(0))
     v = torch.from_numpy(fx["v"])
     f = torch.from_numpy(fx["f"].astype(np.int64))
-    pos, nrm = sample_surface(v, f, n, generator=torch.Generator().manual_seed(0))
+    pos, nrm, fid = sample_surface(v, f, n, generator=torch.Generator().manual_seed(0), return_faces=True)
     assert torch.equal(pos, pc.v) and torch.equal(nrm, pc.n)
-    # the same draws again, keeping the face ids (sample_surface's first RNG use)
-    a32, b32, c32 = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
-    area32 = torch.cross(b32 - a32, c32 - a32, dim=1).norm(dim=1)
-    fid = torch.multinomial(area32 / area32.sum(), n, replacement=True, generator=torch.Generator().manual_seed(0))
     v = v.double()
     a, b, c = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
     cr = torch.cross(b - a, c - a, dim=1)

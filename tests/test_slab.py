@@ -84,19 +84,21 @@ def _free_port():
 
 
 def _worker(rank, world, port, out_path, halo_scale, opts=None):
+    from slab_cpu_engine import CpuSlabEngineDiag
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     opts = dict(opts or {})
     rebalance_after = opts.pop("rebalance_after", None)
+    engine = CpuSlabEngineDiag if opts.pop("diagnostics", False) else CpuSlabEngine
     try:
         pos, nrm = _cloud()
         params, _ = _params(pos)
         tr = TorchTransport()
         # only the coordinator (rank 0) hands in the cloud; the others receive their slab + halo from it
         sd = SlabDenoiser(pos if rank == 0 else None, nrm if rank == 0 else None, max(K, KU), transport=tr, halo=_halo(pos, K) * halo_scale,
-                          engine_factory=CpuSlabEngine, **opts)
+                          engine_factory=engine, **opts)
         owned0 = sd.owned_global.numel()
         halo0 = sd.halo
         if rebalance_after is None:
@@ -118,7 +120,8 @@ def _worker(rank, world, port, out_path, halo_scale, opts=None):
         dist.all_gather(allo, owned)
         if rank == 0:
             np.savez(out_path, pos=p.numpy(), n=n.numpy(), err=int(flag), halo=sd.halo_points, replans=sd.replans,
-                     final_halo=sd.halo, halo0=halo0, owned=torch.stack(allo).numpy())
+                     final_halo=sd.halo, halo0=halo0, owned=torch.stack(allo).numpy(),
+                     log=np.array([repr(x) for x in sd.replan_log]))
     finally:
         dist.destroy_process_group()
 
@@ -170,6 +173,22 @@ def test_slab_world2_thin_halo_replans_and_matches_oracle(tmp_path):
     assert int(res["err"]) == 0
     assert int(res["replans"]) >= 1
     assert float(res["final_halo"]) == pytest.approx(float(res["halo0"]) * 3.0 ** int(res["replans"]), rel=1e-6)
+    _assert_matches_oracle(res)
+
+
+def test_slab_world2_thin_halo_grows_by_the_measured_reach(tmp_path):
+    """With the coverage diagnostics (the engine reports how far the farthest k-ball reached past the band box, as
+    libpcd's pcd_denoiser_coverage_excess does) a re-plan grows the band by 1.5 x that reach (at least x 1.1) instead
+    of x halo_growth: one re-plan covers it, the final band is far below the x 3 growth, and the result is the
+    oracle's."""
+    import ast
+    res = _run_world2(tmp_path, 0.05, {"check_every": 1, "halo_growth": 3.0, "diagnostics": True})
+    assert int(res["err"]) == 0
+    assert int(res["replans"]) == 1, list(res["log"])       # (x 3 growth from the same start: 2 re-plans)
+    log = ast.literal_eval(str(res["log"][0]))
+    assert log["band_failed"] and not log["sphere_failed"] and log["band_excess"] > 0
+    halo0 = float(res["halo0"])
+    assert float(res["final_halo"]) == pytest.approx(max(1.1 * halo0, halo0 + 1.5 * log["band_excess"]), rel=1e-6)
     _assert_matches_oracle(res)
 
 
