@@ -475,9 +475,13 @@ def main():
         dist.broadcast(dt, 0)
         d = float(dt)
         # coverage checked every 10 iterations (a thin halo re-plans and replays, pcd_slab); slabs re-cut by class
-        # cost after the second warm-up iteration (rebalance), so the timed region runs on the balanced plan
+        # cost after the first warm-up iteration (rebalance), so the timed region runs on the balanced plan.  The
+        # first plan covers that one iteration (its k-balls at the snapshot); the re-cut prices the drift measured
+        # over it for every iteration that follows (cut_spheres), so the run needs no coverage re-plan.
+        reb = args.rebalance and args.warmup >= 2
         tr = TorchTransport(rccl=not args.rehearse_one_gpu)
-        sd = SlabDenoiser(pos, nrm, max(args.k, args.k_update), transport=tr, seeding=args.seeding, check_every=10)
+        sd = SlabDenoiser(pos, nrm, max(args.k, args.k_update), transport=tr, seeding=args.seeding, check_every=10,
+                          step_bound=d, horizon=1 if reb else args.warmup + args.steps)
         progress(f"slabs handed out (halo {sd.halo:.4g}); warm-up")
         del pos, nrm
         torch.cuda.empty_cache()
@@ -505,8 +509,9 @@ def main():
             first_ms = (time.perf_counter() - tf) * 1e3
         else:
             step()
-        if mode == "slab" and args.rebalance and w == min(1, args.warmup - 2):
-            sd.rebalance()         # cost-weighted cut from this iteration's classes (next iteration re-anchors)
+        if mode == "slab" and reb and w == 0:
+            # cost-weighted cut from this iteration's classes (the next iteration re-anchors), sized for the rest
+            sd.rebalance(horizon=args.warmup - 1 + args.steps)
             progress("re-cut by class cost")
         if mode == "slab":
             progress(f"warm-up iteration {w + 1}/{args.warmup}")

@@ -437,10 +437,15 @@ class SlabDenoiser:
 
     def __init__(self, snap_pos, snap_n, k_max, transport=None, halo=None, engine_factory=None, seeding=True,
                  k_hint=None, check_every=1, halo_growth=2.0, max_replans=4, weights=None, native=None,
-                 sphere_quantile=0.999):
+                 sphere_quantile=0.999, step_bound=None, horizon=None):
         """native: one pcd_slab_iterate call per iteration over libpcd's own transport (default for the HIP engine);
         False: the same stages driven from Python over torch.distributed.  sphere_quantile: the default halo covers
-        this quantile of the near-face k-ball reaches; the points beyond it keep coverage spheres (cut_spheres)."""
+        this quantile of the near-face k-ball needs; the points beyond it keep coverage spheres (cut_spheres).
+        step_bound: the loop's per-iteration displacement bound (params.d: every step's move is clamped below it),
+        which prices the drift the first plan must cover; horizon: the iterations a plan is sized to cover (default
+        check_every) -- the default halo of every later plan (rebalance, a coverage re-plan) prices each point's
+        measured drift over that many iterations ahead (cut_spheres), so a run of `horizon` iterations needs no
+        coverage re-plan."""
         self.t = transport or LocalTransport()
         rank, world = self.t.rank, self.t.world
         # cell lattice of the ranks' snapshot indices: the fused loop's (pcd_native.fused_k_hint) unless given
@@ -458,13 +463,18 @@ class SlabDenoiser:
         self._sphere_quantile = float(sphere_quantile)
         self._band_floor = 0.0     # the band a coverage failure grew to (a re-cut never goes below it)
         self._sphere_scale = 1.0   # the spheres' growth by coverage failures
+        self.step_bound = float(step_bound) if step_bound else 0.0
+        self.horizon = int(horizon) if horizon else max(int(check_every), 1)
+        self.iterations_done = 0   # iterations since load (the drift estimate's clock)
+        self._ckpt_iter = 0
         if rank == 0:
             self.snap_pos, self.snap_n = snap_pos.detach().contiguous(), snap_n.detach().contiguous()
             self.dev = self.snap_pos.device
             self._spheres = None
             if halo is None:
                 if world > 1:
-                    halo, sid, srad = cut_spheres(self.snap_pos, world, k_max, quantile=sphere_quantile, weights=weights)
+                    halo, sid, srad = cut_spheres(self.snap_pos, world, k_max, quantile=sphere_quantile, weights=weights,
+                                                  step=self.step_bound, horizon=self.horizon)
                     self._spheres = Spheres.around(self.snap_pos, sid, srad) if engine_factory is None else None
                 else:
                     halo = 0.0
@@ -607,22 +617,27 @@ class SlabDenoiser:
         g = self._gather_to0(torch.cat([owned_pos, owned_n], 1))
         return None if g is None else (g[:, :3], g[:, 3:])
 
-    def _replan(self, halo=None, weights=None, state="now", sphere_scale=None):
+    def _replan(self, halo=None, weights=None, state="now", sphere_scale=None, at=None, horizon=None):
         """Re-cut every rank from the frozen snapshot, taking over `state` (global current pos, n on the
-        coordinator, None on the other ranks; "now": gather the present iterate).  halo / sphere_scale (coordinator):
-        the grown band and the factor for the coverage spheres (None: unchanged); weights: a new cost-weighted cut --
-        with the default halo its band and spheres are recomputed for the new faces (the old cut's spheres would
-        miss the sparse points near the moved cuts).  Collective: all ranks call it together."""
+        coordinator, None on the other ranks, reached after `at` iterations; "now": gather the present iterate).
+        halo / sphere_scale (coordinator): the grown band and the factor for the coverage spheres (None: unchanged);
+        weights: a new cost-weighted cut.  With the default halo the band and the spheres are recomputed for the
+        state's positions and the drift of `horizon` iterations ahead (cut_spheres: a moved cut has new sparse points
+        near it, and the drift since the snapshot has moved every ball), never below `halo`.  Collective: all ranks
+        call it together."""
         if isinstance(state, str):
             state = self._global_state(*self._owned_state_now())
+            at = self.iterations_done
         plan = None
         if self.t.rank == 0:
             if weights is not None:
                 self._weights = weights
-            if weights is not None and self._auto_halo:
+            if self._auto_halo:
                 band, sid, srad = cut_spheres(self.snap_pos, self.t.world, self.k_max, quantile=self._sphere_quantile,
-                                              axis=self.plan.axis, weights=self._weights)
-                halo = max(band, self._band_floor)
+                                              axis=self.plan.axis, weights=self._weights,
+                                              query=None if state is None else state[0], iterations=at or 0,
+                                              step=self.step_bound, horizon=horizon or self.horizon)
+                halo = max(band, self._band_floor, halo or 0.0)
                 self._spheres = Spheres.around(self.snap_pos, sid, srad * self._sphere_scale)
             else:
                 if sphere_scale is not None and self._spheres is not None:
@@ -688,7 +703,8 @@ class SlabDenoiser:
             gstate = self._global_state(*self._ckpt)
             before = self.halo
             self._replan(halo if self.t.rank == 0 else None, state=gstate,
-                         sphere_scale=scale if self.t.rank == 0 else None)
+                         sphere_scale=scale if self.t.rank == 0 else None, at=self._ckpt_iter,
+                         horizon=max(self.horizon, len(self._pending)))
             self.replan_log.append(dict(why, reason="coverage", halo_before=before, halo_after=self.halo,
                                         sphere_scale=scale))
             if self.t.rank == 0:
@@ -744,8 +760,10 @@ class SlabDenoiser:
         for _ in range(iterations):
             if self.check_every > 0 and self._ckpt is None:
                 self._ckpt = self._owned_state_now()
+                self._ckpt_iter = self.iterations_done
                 self._pending = []
             self._one(params)
+            self.iterations_done += 1
             if self.check_every > 0:
                 self._pending.append(params)
                 self._since += 1
@@ -765,12 +783,13 @@ class SlabDenoiser:
         self.verify()
         if self.check_every > 0:
             self._ckpt = self._owned_state_now()
+            self._ckpt_iter = self.iterations_done
 
-    def rebalance(self, class_weights=(1.0, 1.3, 1.4)):
+    def rebalance(self, class_weights=(1.0, 1.3, 1.4), horizon=None):
         """Re-cut the slabs by cost: each point weighs class_weights[its class in the last NVT2 stage] (flat, edge,
         corner: the edge / feature steps solve a 3x3 system over their neighbours).  Collective.  Iterations since the
         last coverage check are verified first (a thin halo there re-plans and replays them), so the state carried
-        into the new cut is exact."""
+        into the new cut is exact.  horizon: the iterations the new plan is sized to cover (default self.horizon)."""
         self.verify()
         cls = self.e.classes()
         cls = cls[self.owned_local.to(cls.device)]
@@ -778,7 +797,7 @@ class SlabDenoiser:
         w_own = w_tab[cls.clamp(0, len(class_weights) - 1)]
         weights = self._gather_to0(w_own[:, None])
         before = self.halo
-        self._replan(weights=None if weights is None else weights[:, 0].to(self.snap_pos.device))
+        self._replan(weights=None if weights is None else weights[:, 0].to(self.snap_pos.device), horizon=horizon)
         self.replan_log.append({"reason": "rebalance", "halo_before": before, "halo_after": self.halo})
         self._since, self._pending, self._ckpt = 0, [], None
 
@@ -815,34 +834,58 @@ class SlabDenoiser:
         return self.owned_global, pos[idx], n[idx]
 
 
+def _quantile(x: torch.Tensor, q: float) -> float:
+    """(torch.quantile refuses inputs past 16M elements)"""
+    return float(torch.sort(x).values[int(q * (x.numel() - 1))]) if x.numel() else 0.0
+
+
 def cut_spheres(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, quantile: float = 0.999,
-                axis: int | None = None, sphere_margin: float = 1.5, weights: torch.Tensor | None = None):
+                axis: int | None = None, sphere_margin: float = 1.5, weights: torch.Tensor | None = None,
+                query: torch.Tensor | None = None, iterations: int = 0, step: float = 0.0, horizon: int = 1,
+                speed_floor: float = 0.99):
     """(band halo, sphere centre ids, sphere radii) for the cut SlabPlan.build makes with the same `weights` (None:
-    equal counts): the band is `margin` x the `quantile` of the near-face reaches (cut_halo's per-point requirement);
-    every point whose ball reaches farther keeps a sphere of radius sphere_margin x d_k around itself instead (all of
-    its snapshot members local to its owner), so a few sparse points near a cut no longer set every rank's halo (at
-    80M points on 8 ranks the max-reach halo held ~half as many halo rows as owned ones).  A cost-weighted re-cut
-    moves the faces, so the band and the spheres are recomputed for it (SlabDenoiser._replan)."""
-    idx, reach, dk = _cut_reach(snap_pos, world, k, axis, weights)
+    equal counts), covering the next `horizon` iterations from the state `query` (the current positions after
+    `iterations` iterations; None: the snapshot itself).
+
+    Each near-face point needs its k-ball's reach past its slab's faces now, plus the drift of the iterations ahead:
+    need = reach + (horizon - 1) x v, with v its own mean speed so far (displacement from the snapshot / iterations)
+    plus a floor (the `speed_floor` quantile of those speeds: a point that has not moved yet may start to), or, before
+    any iteration, `step` (the loop's per-iteration displacement bound: every step's move is clamped below d,
+    Denoiser.py's `norm < d` keeps).  The band is `margin` x the `quantile` of the needs; every point that needs
+    more keeps a sphere around its snapshot position instead (all its snapshot members local to its owner), of
+    radius 1.1 x (displacement + d_k + twice the drift ahead) -- the triangle inequality's bound on |q - o| + d_k(q)
+    -- and at least sphere_margin x d_k.  So a few sparse or fast-moving points near a cut do not set every rank's
+    halo.  Measured on configs[4]'s 80M cloud (tools/halo_policy_probe.py, 8 slabs): planned after iteration 1 for
+    iterations 2..8 this fails no row.  A cost-weighted re-cut moves the faces, so the band and the spheres are
+    recomputed for it (SlabDenoiser._replan)."""
+    idx, reach, dk, disp = _cut_reach(snap_pos, world, k, axis, weights, query=query)
     if idx.numel() == 0:
         z = torch.zeros(0, dtype=torch.int64)
         return 0.0, z, torch.zeros(0)
-    r = reach.clamp(min=0)
-    rs = torch.sort(r).values                        # (torch.quantile refuses inputs past 16M elements)
-    band = margin * max(float(rs[int(quantile * (rs.numel() - 1))]), float(torch.sort(dk).values[dk.numel() // 2]))
-    out = margin * r > band
-    return band, idx[out], sphere_margin * dk[out]
+    ahead = max(int(horizon) - 1, 0)
+    if iterations > 0:
+        s = disp / float(iterations)
+        grow = ahead * (s + _quantile(s, speed_floor))
+    else:
+        grow = torch.full_like(reach, ahead * float(step))
+    need = (reach + grow).clamp(min=0)
+    band = margin * max(_quantile(need, quantile), _quantile(dk, 0.5))
+    out = margin * need > band
+    radii = torch.maximum(sphere_margin * dk, 1.1 * (disp + dk + 2 * grow))
+    return band, idx[out], radii[out]
 
 
 def _cut_reach(snap_pos: torch.Tensor, world: int, k: int, axis: int | None = None,
-               weights: torch.Tensor | None = None, chunk: int = 8_000_000):
+               weights: torch.Tensor | None = None, chunk: int = 8_000_000, query: torch.Tensor | None = None):
     """Per point near a face of the cut (_cut with `weights`): (global id, reach of its k-ball past its slab's faces,
-    d_k).  'Near' = within default_halo of a face (the sampled bound, the quantile's population) OR any point whose
-    own k-ball crosses a face: d_k comes from every point (in chunks), so a sparse outlier far from a face with a
-    ball past it -- which a sampled bound misses -- is priced too (round 6: the 80M / 8-rank rehearsal's first
-    iteration failed its coverage check on such points)."""
+    d_k, displacement from the snapshot), the ball centred at its `query` position (None: the snapshot; the kNN is
+    over the snapshot, as K1 searches).  'Near' = within default_halo of a face (the sampled bound, the quantile's
+    population) OR any point whose own k-ball crosses a face: d_k comes from every point (in chunks), so a sparse
+    outlier far from a face with a ball past it -- which a sampled bound misses -- is priced too (round 6: the 80M /
+    8-rank rehearsal's first iteration failed its coverage check on such points)."""
     dev = nat.device()
     pos = snap_pos.to(dev)
+    qpos = pos if query is None else query.to(dev, torch.float32)
     axis, key, rank_of, lo, hi = _cut(pos, world, axis, None if weights is None else weights.to(dev))
     band = default_halo(pos, k)
     lo_t = torch.tensor(lo, device=dev, dtype=key.dtype)[rank_of]
@@ -852,15 +895,18 @@ def _cut_reach(snap_pos: torch.Tensor, world: int, k: int, axis: int | None = No
     n = pos.size(0)
     dk = torch.empty(n, dtype=torch.float32, device=dev)
     for c0 in range(0, n, chunk):
-        _, d2 = g.knn(pos[c0:c0 + chunk].contiguous(), k, with_d2=True, idx_bits=32)
+        _, d2 = g.knn(qpos[c0:c0 + chunk].contiguous(), k, with_d2=True, idx_bits=32)
         dk[c0:c0 + chunk] = d2[:, -1].sqrt()
         del d2
-    up = torch.where(last, torch.zeros_like(dk), key + dk - hi_t)
-    down = torch.where(first, torch.zeros_like(dk), lo_t - key + dk)
+    qk = qpos[:, axis]
+    up = torch.where(last, torch.zeros_like(dk), qk + dk - hi_t)
+    down = torch.where(first, torch.zeros_like(dk), lo_t - qk + dk)
     reach = torch.maximum(up, down)
-    near = ((key > hi_t - band) & ~last) | ((key < lo_t + band) & ~first) | (reach > 0)
+    near = ((qk > hi_t - band) & ~last) | ((qk < lo_t + band) & ~first) | (reach > 0)
     idx = torch.nonzero(near).flatten()
-    return idx, reach[idx], dk[idx]
+    disp = torch.zeros(idx.numel(), dtype=torch.float32, device=dev) if query is None else \
+        (qpos[idx] - pos[idx]).norm(dim=1)
+    return idx, reach[idx], dk[idx], disp
 
 
 def cut_halo(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, axis: int | None = None,
@@ -874,7 +920,7 @@ def cut_halo(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, a
     later ball that leaves the halo (a re-plan widens it)."""
     if world == 1:
         return 0.0
-    idx, reach, _ = _cut_reach(snap_pos, world, k, axis, weights)
+    idx, reach, _, _ = _cut_reach(snap_pos, world, k, axis, weights)
     if idx.numel() == 0:
         return 0.0
     return margin * float(reach.max().clamp(min=0))

@@ -30,7 +30,7 @@ def main():
     plan = SlabPlan.build(pos, world, band, spheres=Spheres.around(pos, sid, srad))
     own = torch.bincount(plan.owner, minlength=world)
     halo_rows = max(int(plan.local[r].numel() - own[r]) for r in range(world))
-    idx, reach0, dk0 = _cut_reach(pos, world, 32)
+    idx, reach0, dk0, _ = _cut_reach(pos, world, 32)
     axis, key, owner, lo, hi = _cut(pos, world)
     lo_t = torch.tensor(lo, device=dev)[owner[idx]]
     hi_t = torch.tensor(hi, device=dev)[owner[idx]]
