@@ -545,7 +545,9 @@ def main():
             sd.checkpoint()
             sd.check_every = args.steps + 1
             replans = sd.replans
+            rs0 = sd.e.readset_stats() if hasattr(sd.e, "readset_stats") else (0, 0, 0)
             elapsed = timed_region()
+            rs1 = sd.e.readset_stats() if hasattr(sd.e, "readset_stats") else (0, 0, 0)
             sd.verify()
             sd.check_every = every
             if sd.replans == replans:
@@ -705,16 +707,38 @@ def main():
         counts = torch.tensor([sd.owned_global.numel(), sd.halo_points], dtype=torch.int64)
         allc = [torch.zeros_like(counts) for _ in range(world)]
         dist.all_gather(allc, counts)
-        # halo traffic: every received halo row is refreshed once per exchange -- f_n after K1, then the positions
+        # halo traffic with every held halo row refreshed once per exchange -- f_n after K1, then the positions
         # after each Gauss-Seidel phase (once per iteration in the Jacobi mode) -- as 12-byte rows on the RCCL path
         n_x = 1 + (1 if params.jacobi else params.nphases)
-        xb = [int(c[1]) * 12 * n_x for c in allc]
+        xb_all = [int(c[1]) * 12 * n_x for c in allc]
+        # the read-set exchange (pcd_denoiser_set_readset, the default): per iteration only the halo rows some own
+        # list reads -- position + normal with the K1 refresh (24 B), f_n (12 B), positions after every phase but
+        # the last (12 B each) -- plus one mask bit per held halo row; rows averaged over the timed iterations
+        if rs1[0] < rs0[0]:          # (a re-plan inside the region: a new engine, its stats restarted)
+            rs0 = (0, 0, 0)
+        its = rs1[0] - rs0[0]
+        rd = torch.tensor([(rs1[2] - rs0[2]) / its if its else -1.0], dtype=torch.float64)
+        alld = [torch.zeros_like(rd) for _ in range(world)]
+        dist.all_gather(alld, rd)
+        read_rows = [float(x) for x in alld]
+        per_row = 24 + 12 + (0 if params.jacobi else 12 * (params.nphases - 1))
+        if its:
+            xb = [int(r * per_row + int(c[1]) / 8) for r, c in zip(read_rows, allc)]
+        else:
+            xb = xb_all
         out["slab"] = {"world": info["world"], "transport": info["transport"],
                        "owned_rows": [int(c[0]) for c in allc], "halo_rows": [int(c[1]) for c in allc],
+                       "read_rows_per_iteration": [round(r, 1) for r in read_rows] if its else None,
+                       "readset": bool(its),
                        "halo": sd.halo, "replans": sd.replans, "replan_log": sd.replan_log,
-                       "exchanges_per_iteration": n_x, "exchange_bytes_per_iteration": sum(xb),
+                       "exchanges_per_iteration": (1 + 1 + (0 if params.jacobi else params.nphases - 1)) if its
+                       else n_x,
+                       "exchange_bytes_per_iteration": sum(xb),
                        "exchange_bytes_per_iteration_max_rank": max(xb),
+                       "exchange_bytes_per_iteration_all_halo_rows": sum(xb_all),
                        "exchange_ms": None if xchg is None else round(xchg, 4),
+                       "exchange_ms_kind": "one FIELD_POS refresh of every held halo row (pcd_halo_exchange), "
+                                           "median of 5, max over ranks",
                        "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
                        "note": ("every rank on GPU 0 over libpcd's host transport: a rehearsal, not a scaling number"
                                 if args.rehearse_one_gpu else

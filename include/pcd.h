@@ -359,6 +359,16 @@ int pcd_halo_exchange(pcd_denoiser* dn, pcd_comm* c, int field, void* stream);
  * overlapped with the rows that need no halo data (the exchange runs on a stream of the library's own; later
  * calls on this denoiser wait for it).  Same result bit for bit as the staged sequence above. */
 int pcd_slab_iterate(pcd_denoiser* dn, pcd_comm* c, const pcd_denoise_params* p, int iterations, void* stream);
+/* Read-set exchange (on by default; PCD_SLAB_READSET=0 in the environment at pcd_denoiser_set_routes, or on = 0
+ * here: every halo row in every exchange).  pcd_slab_iterate's K1 stores the kNN lists first; each rank marks the
+ * halo rows the lists of its band rows (k-ball not inside the owned slab) hold, sends that mask to each peer (one bit
+ * per route row), and the peers send position + normal of exactly those rows while NVT1 runs the no-halo rows; the
+ * iteration's f_n and position exchanges move the same rows, and no exchange trails the iteration.  The halo rows a
+ * list does not hold are not kept current (pcd_halo_exchange refreshes every one).  Needs the anchored K1 (list cap
+ * <= 32, seeding and anchoring on) and >= 2k local rows on every rank. */
+int pcd_denoiser_set_readset(pcd_denoiser* dn, int on);
+/* since pcd_denoiser_set_routes: read-set iterations and the send / receive rows they moved, summed */
+int pcd_denoiser_readset_stats(const pcd_denoiser* dn, int64_t* iterations, int64_t* send_rows, int64_t* recv_rows);
 
 /* ------------------------------------------------------------------ normal orientation (host) */
 /* GraphBuilder.flipNormals: Kruskal MST on cost 1-|n_i·n_j| over the directed edge list (a[e] -> b[e],

@@ -17,6 +17,7 @@
 // exchange between stages (pcd_denoiser_pack/unpack), and the global flat centre / delta reductions are exposed as
 // separate stages so the caller can all-reduce them (pcd_denoiser_stage).  pcd_denoiser_iterate is the same stage
 // sequence with no exchange.
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -545,12 +546,13 @@ template <int K, bool UNIT>
 __global__ __launch_bounds__(kNvtBS, PCD_NVT1_OCC) void k_nvt1(GridView g, const float4* __restrict__ pos, const float4* __restrict__ nrm,
                                                const int32_t* __restrict__ idx, int64_t N, RowMap rm, int k,
                                                int kstore, float rho, float tau, float damp, Cover cov,
-                                               float4* __restrict__ fn, int* __restrict__ err, int win, Band band) {
+                                               float4* __restrict__ fn, int* __restrict__ err, int win, Band band,
+                                               RowSel sel) {
     __shared__ float4 s_pos[kWinRows], s_nrm[kWinRows];
     const int64_t b0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
     const int64_t lo = stage_window(pos, nrm, N, rm(b0), s_pos, s_nrm, win);
     const int64_t t0 = b0 + threadIdx.x;
-    if (t0 >= rm.nq) return;
+    if (t0 >= rm.nq || !sel.take(t0)) return;
     nvt1_row<K, UNIT>(g, pos, nrm, idx, N, rm(t0), k, kstore, rho, tau, damp, cov, fn, err, WinRows<>{pos, s_pos, lo},
                 WinRows<>{nrm, s_nrm, lo}, band, t0);
 }
@@ -1004,6 +1006,19 @@ struct pcd_denoiser {
     bool xpending = false;        // xev_out marks an exchange the state's next reader must wait for
     bool xbegun = false;          // host transport: packed, callback not yet run
     XField xfield{};
+    // read-set exchange (pcd_slab.h): each iteration moves only the halo rows some own row's list reads
+    bool readset = true;          // on by default (PCD_SLAB_READSET=0: every halo row, every exchange)
+    bool use_sel = false;         // the exchanges of this iteration use the selected routes
+    int32_t* rpos = nullptr;      // local row -> its index in rrows, -1: not a halo row
+    uint8_t* rmark = nullptr;     // per receive-route row: read by some own row's list
+    uint32_t *rwords = nullptr, *swords = nullptr, *wpopc = nullptr, *wscan = nullptr;
+    int32_t *sel_srows = nullptr, *sel_rrows = nullptr;
+    int64_t* xoff_d = nullptr;    // device: roff, soff, rwoff, swoff (npeers + 1 each)
+    int64_t* seloff_d = nullptr;  // device: selected receive / send offsets (npeers + 1 each)
+    int64_t* seloff_h = nullptr;  // pinned host copy
+    std::vector<int64_t> rwoff{0}, swoff{0}, sel_soff{0}, sel_roff{0};
+    hipEvent_t rs_ev = nullptr;
+    int64_t rs_iters = 0, rs_send_rows = 0, rs_recv_rows = 0;   // read-set iterations and their summed row counts
     // CPSD driver (pcd_cpsd.h): radius member rows, member counts, overflow flag
     bool nvt1_on = true;          // K1 runs NVT1 after the kNN (off: the lists only)
     int32_t* ckeys = nullptr;                            // [cpsd_cap][nq] member rows (slot-major), ascending original index
@@ -1063,7 +1078,7 @@ static bool phase_is_global(const pcd_denoise_params* p, int ph) {
 #endif
 static const Band kNoBand{Cover{{1.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, nullptr};
 static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int K, hipStream_t st,
-                             hipEvent_t* ev, const Band& band, hipEvent_t before_nvt1) {
+                             hipEvent_t* ev, const Band& band, hipEvent_t before_nvt1, bool lists_only) {
     const int64_t N = dn->n;
     const RowMap rm = dn->rowmap();
     const int kstore = std::max(p->k, p->k_update);
@@ -1120,14 +1135,14 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
                            dn->alist, dn->idx, dn->spill, spill_cnt, dn->err);                                         \
         if (ev) PCD_HIP(hipEventRecord(ev[3], st));                                                                    \
         if (before_nvt1) PCD_HIP(hipStreamWaitEvent(st, before_nvt1, 0));                                              \
-        if (!dn->nvt1_on) {                                                                                            \
-            /* the kNN lists only (the CPSD driver's update selection, pcd_cpsd.h) */                                   \
+        if (!dn->nvt1_on || lists_only) {                                                                              \
+            /* the kNN lists only (the CPSD driver's update selection, pcd_cpsd.h; the slabs' read-set exchange) */   \
         } else if (dn->unit_nrm) {                                                                                     \
             hipLaunchKernelGGL((k_nvt1<C, true>), grd_nvt, blk_nvt, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,       \
-                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, band);                  \
+                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, band, RowSel{nullptr, 0});  \
         } else {                                                                                                       \
             hipLaunchKernelGGL((k_nvt1<C, false>), grd_nvt, blk_nvt, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore,      \
-                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, band);                  \
+                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, band, RowSel{nullptr, 0});  \
         }                                                                                                              \
         break;
     switch (K) {
@@ -1141,17 +1156,23 @@ static int stage_k1_anchored(pcd_denoiser* dn, const pcd_denoise_params* p, int 
     return PCD_OK;
 }
 
+// K1 takes the anchored path (its kNN and NVT1 are separate launches)
+static bool k1_anchored(const pcd_denoiser* dn, const pcd_denoise_params* p) {
+    const int K = list_cap(p);
+    return dn->rowmap().nq > 0 && dn->seeding && dn->anchoring && K <= 32 && dn->n >= 2 * K && knn_cap(dn->kcap) <= 32;
+}
+
 // band: spatial slabs, mark the rows that may read a halo row (pcd_slab_iterate); before_nvt1: an event the
 // neighbour gathers must wait for (the previous iteration's position exchange; the kNN itself reads only the row's
-// own position and the frozen snapshot).
+// own position and the frozen snapshot).  lists_only (anchored path): the kNN lists, NVT1 left to stage_nvt1.
 static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t st, hipEvent_t* ev = nullptr,
-                    const Band& band = kNoBand, hipEvent_t before_nvt1 = nullptr) {
+                    const Band& band = kNoBand, hipEvent_t before_nvt1 = nullptr, bool lists_only = false) {
     const int64_t N = dn->n;
     const RowMap rm = dn->rowmap();
     const int kstore = std::max(p->k, p->k_update);
     const int K = list_cap(p);
-    if (rm.nq > 0 && dn->seeding && dn->anchoring && K <= 32 && N >= 2 * K && knn_cap(dn->kcap) <= 32)
-        return stage_k1_anchored(dn, p, K, st, ev, band, before_nvt1);
+    if (k1_anchored(dn, p)) return stage_k1_anchored(dn, p, K, st, ev, band, before_nvt1, lists_only);
+    if (lists_only) return fail(PCD_ERR_ARG, "stage_k1: lists only needs the anchored path");
     if (ev) for (int e = 1; e <= 3; ++e) PCD_HIP(hipEventRecord(ev[e], st));   // no anchored sub-stages
     if (before_nvt1) PCD_HIP(hipStreamWaitEvent(st, before_nvt1, 0));         // (the fused kernel gathers at once)
     if (rm.nq == 0) return PCD_OK;
@@ -1171,6 +1192,33 @@ static int stage_k1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t s
 #undef PCD_K1
     PCD_LAUNCH_CHECK();
     dn->seed_cols = dn->list_cols = kstore;
+    return PCD_OK;
+}
+
+// NVT1 + eigh + VU smoothing over the stored lists of the rows `sel` takes (after a lists-only K1)
+static int stage_nvt1(pcd_denoiser* dn, const pcd_denoise_params* p, hipStream_t st, RowSel sel) {
+    const RowMap rm = dn->rowmap();
+    if (rm.nq == 0) return PCD_OK;
+    const int64_t N = dn->n;
+    const int kstore = std::max(p->k, p->k_update);
+    const GridView gv = dn->g->view;
+    float4* P = dn->pos[dn->cur];
+    const dim3 blk_nvt(kNvtBS), grd_nvt((unsigned)cdiv(rm.nq, kNvtBS));
+#define PCD_NV(C)                                                                                                      \
+    case C:                                                                                                            \
+        if (dn->unit_nrm)                                                                                              \
+            hipLaunchKernelGGL((k_nvt1<C, true>), grd_nvt, blk_nvt, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k, kstore, \
+                               p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, kNoBand, sel);          \
+        else                                                                                                           \
+            hipLaunchKernelGGL((k_nvt1<C, false>), grd_nvt, blk_nvt, 0, st, gv, P, dn->nrm, dn->idx, N, rm, p->k,      \
+                               kstore, p->rho, p->tau, p->damp, dn->cov, dn->fn, dn->err, dn->windows, kNoBand, sel);  \
+        break;
+    switch (list_cap(p)) {
+        PCD_NV(8) PCD_NV(16) PCD_NV(32)
+        default: return fail(PCD_ERR_ARG, "unsupported k");
+    }
+#undef PCD_NV
+    PCD_LAUNCH_CHECK();
     return PCD_OK;
 }
 

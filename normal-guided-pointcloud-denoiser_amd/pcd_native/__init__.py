@@ -120,6 +120,8 @@ _SIGS = {
     "pcd_denoiser_set_routes": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p]),
     "pcd_halo_exchange": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "pcd_denoiser_set_readset": (c_int, [c_void_p, c_int]),
+    "pcd_denoiser_readset_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
     "pcd_slab_iterate": (c_int, [c_void_p, c_void_p, POINTER(DenoiseParams), c_int, c_void_p]),
     "pcd_orient_normals_mst": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64]),
     "pcd_orient_normals_mst_gpu": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p]),
@@ -479,6 +481,17 @@ class FusedDenoiser:
     def halo_exchange(self, comm: "Comm", field: int):
         check(lib().pcd_halo_exchange(self.handle, comm.handle, int(field), c_void_p(stream_ptr())),
               "pcd_halo_exchange")
+
+    def set_readset(self, on: bool):
+        """slab_iterate moves only the halo rows the lists read (pcd_denoiser_set_readset; default on)."""
+        check(lib().pcd_denoiser_set_readset(self.handle, int(bool(on))), "pcd_denoiser_set_readset")
+
+    def readset_stats(self) -> tuple:
+        """(iterations, send rows, receive rows) of the read-set exchange since set_routes, summed."""
+        it, s, r = c_int64(0), c_int64(0), c_int64(0)
+        check(lib().pcd_denoiser_readset_stats(self.handle, ctypes.byref(it), ctypes.byref(s), ctypes.byref(r)),
+              "pcd_denoiser_readset_stats")
+        return it.value, s.value, r.value
 
     TIMING_SLOTS = ("anchor_test", "requery", "spill_search", "nvt1", "nvt2", "flat_phase", "edge_phase",
                     "corner_phase", "finish")

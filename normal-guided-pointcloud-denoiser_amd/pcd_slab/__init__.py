@@ -321,6 +321,10 @@ class HipSlabEngine:
     def slab_iterate(self, comm, params, iterations=1):
         self.fused.slab_iterate(comm, params, iterations)
 
+    def readset_stats(self) -> tuple:
+        """(iterations, send rows, receive rows) of the read-set exchange since the routes were set (summed)."""
+        return self.fused.readset_stats()
+
     def slab_iterate_timed(self, comm, params) -> dict:
         """One slab iteration with the library's per-stage HIP events (pcd_denoiser_set_timing), ms."""
         self.fused.set_timing(True)

@@ -65,7 +65,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=False, native=None, sq=0.999):
+def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=False, native=None, sq=0.999,
+            readset=True):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -84,12 +85,16 @@ def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=F
         if native is not False:
             assert sd.comm.info() == {"world": world, "rank": rank,
                                       "transport": "rccl" if backend == "rccl" else "host"}
+        if sd.native and not readset:
+            sd.e.fused.set_readset(False)
         sd.iterate(_params(d, jacobi), ITERS)
         sd.check()
+        rs = sd.e.readset_stats() if sd.native else (0, 0, 0)
         p, n = gather_global(sd.owned_state(), sd.n_total, tr)
         if rank == 0:
             np.savez(out_path, pos=p.numpy(), n=n.numpy(), halo=sd.halo_points, replans=sd.replans,
-                     spheres=0 if sd.plan.spheres is None else int(sd.plan.spheres.ids.numel()))
+                     spheres=0 if sd.plan.spheres is None else int(sd.plan.spheres.ids.numel()),
+                     rs_iters=rs[0], rs_recv=rs[2])
     finally:
         dist.destroy_process_group()
 
@@ -143,6 +148,30 @@ def test_hip_slab_world2_one_call_equals_staged(gpu, tmp_path, jacobi):
         mp.spawn(_worker, args=(2, _free_port(), out, cloud, d, "gloo", jacobi, native), nprocs=2, join=True)
         got[native] = np.load(out)
     assert int(got[True]["halo"]) > 0
+    np.testing.assert_array_equal(got[True]["pos"], got[False]["pos"])
+    np.testing.assert_array_equal(got[True]["n"], got[False]["n"])
+
+
+@pytest.mark.gpu
+def test_hip_slab_world4_readset_equals_every_row(gpu, tmp_path):
+    """The read-set exchange (pcd_denoiser_set_readset, the default: after the kNN each rank asks its peers for the
+    halo rows its lists hold, and every exchange of the iteration moves only those) against every halo row in every
+    exchange: bit-identical, with fewer rows moved than held."""
+    import torch.multiprocessing as mp
+    pos, nrm = _cloud(gpu)
+    d = _d(pos)
+    cloud = str(tmp_path / "cloud.npz")
+    np.savez(cloud, pos=pos.cpu().numpy(), n=nrm.cpu().numpy())
+    got = {}
+    for rs in (True, False):
+        out = str(tmp_path / f"slab4_rs{rs}.npz")
+        mp.spawn(_worker, args=(4, _free_port(), out, cloud, d, "gloo", False, None, 0.999, rs), nprocs=4, join=True)
+        got[rs] = np.load(out)
+    assert int(got[True]["replans"]) == 0 and int(got[False]["replans"]) == 0
+    assert int(got[True]["rs_iters"]) == ITERS and int(got[False]["rs_iters"]) == 0
+    read = int(got[True]["rs_recv"]) / ITERS
+    report(f"read-set exchange, rank 0: {read:.0f} of {int(got[True]['halo'])} held halo rows moved per iteration")
+    assert 0 < read < int(got[True]["halo"])
     np.testing.assert_array_equal(got[True]["pos"], got[False]["pos"])
     np.testing.assert_array_equal(got[True]["n"], got[False]["n"])
 
