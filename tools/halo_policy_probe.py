@@ -78,8 +78,21 @@ def main():
         print(f"  {tag}: band {band:.4g} ({band / d:.2f} d), spheres {int(sph.sum()):,}, failing band rows {bad_band:,}, "
               f"sphere ratio max {ratio:.3f}, halo rows/rank {halo:,}", flush=True)
 
+    # how the need grows after iteration 1, by the row's displacement in iteration 1 (s1, units of d)
+    s1 = D[2] / d
+    bins = [(0.0, 0.05), (0.05, 0.1), (0.1, 0.25), (0.25, 0.5), (0.5, 0.75), (0.75, 1.01)]
+    for lo_, hi_ in bins:
+        m_ = (s1 >= lo_) & (s1 < hi_) & (R[2] > -1e8)
+        if not bool(m_.any()):
+            continue
+        row = []
+        for j in range(4, iters + 1, 3):
+            gr = (R[j] - R[2])[m_] / d
+            gs = (D[j] + K[j] - K[2])[m_] / d
+            row.append(f"j{j}: reach +{q(gr, 0.999):.2f}/{float(gr.max()):.2f} ball {q(gs, 0.999):.2f}/{float(gs.max()):.2f}")
+        print(f"s1 in [{lo_}, {hi_}) d ({int(m_.sum()):,} rows): " + "; ".join(row), flush=True)
     # cut_spheres' policy (g 1, floor q0.99, spheres of 1.1 x (D + d_k + rf x grow)) at band quantiles bq
-    for t, h in ((1, 7),):
+    for t, h in ((1, 7), (1, iters - 1)):
         print(f"plan after iteration {t}, covering iterations {t + 1}..{t + h}:", flush=True)
         need_now = R[t + 1]                 # reach at the plan's state (the query of iteration t+1)
         k_now, d_now = K[t + 1], D[t + 1]
