@@ -281,6 +281,15 @@ class Grid:
         names = ["cells_considered", "cells_probed", "cells_found", "candidates", "inserts", "extra_rings"]
         return {nm: round(float(x), 2) for nm, x in zip(names, v)}
 
+    def radius_counts(self, q: torch.Tensor, radii: torch.Tensor) -> torch.Tensor:
+        """Member counts of the balls of radii[i] around q[i] (pcd_radius_count), int64 [nq]."""
+        q = f32(q)
+        r = f32(radii)
+        counts = torch.empty(q.size(0), dtype=torch.int64, device=q.device)
+        check(lib().pcd_radius_count(self.handle, ptr(q), q.size(0), ptr(r), ptr(counts), c_void_p(stream_ptr())),
+              "pcd_radius_count")
+        return counts
+
     def radius(self, q: torch.Tensor, radii: torch.Tensor):
         """Members of the ball of radii[i] around q[i] (original snapshot ids, ascending): (slices int64 [nq+1],
         j int64 [total]) -- scipy query_ball_point semantics (pcd_radius_count / pcd_radius_fill)."""

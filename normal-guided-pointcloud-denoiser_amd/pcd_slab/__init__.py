@@ -74,26 +74,40 @@ def _cut(snap: torch.Tensor, world: int, axis: int | None = None, weights: torch
 @dataclass
 class Spheres:
     """Coverage spheres of the sparse points near a cut (cut_spheres): centre ids (global), radii, and the snapshot
-    members of each sphere (CSR over the centres, global ids) -- local to the centre's owner."""
+    members each centre's owner must hold -- per owner rank, the union of its spheres' members (global ids, unique),
+    so a plan holds them whatever the spheres' overlap."""
     ids: torch.Tensor
     radii: torch.Tensor
-    slices: torch.Tensor
-    members: torch.Tensor
+    by_rank: dict
 
     @staticmethod
-    def around(snap: torch.Tensor, ids: torch.Tensor, radii: torch.Tensor, k_hint: int = 16) -> "Spheres":
+    def around(snap: torch.Tensor, ids: torch.Tensor, radii: torch.Tensor, owner: torch.Tensor, k_hint: int = 16,
+               chunk_members: int = 32_000_000) -> "Spheres":
+        """owner: [N] rank of every snapshot point (the plan's cut).  The members are found a chunk of centres at a
+        time (at most ~chunk_members pairs in flight), so wide spheres -- a long planned horizon -- stay bounded in
+        memory."""
         dev = nat.device()
         if ids.numel() == 0:
-            z = torch.zeros(0, dtype=torch.int64, device=snap.device)
-            return Spheres(z, torch.zeros(0, device=snap.device), torch.zeros(1, dtype=torch.int64, device=snap.device), z)
+            return Spheres(ids.to(snap.device), torch.zeros(0, device=snap.device), {})
         g = nat.Grid(snap.to(dev), k_hint=k_hint)
+        q = snap.to(dev)[ids.to(dev)].contiguous()
         # (membership at a hair over the radius: the coverage test asks for the ball strictly inside it)
-        sl, j = g.radius(snap.to(dev)[ids.to(dev)].contiguous(), (radii.to(dev) * 1.0001).contiguous())
-        return Spheres(ids.to(snap.device), radii.to(snap.device, torch.float32), sl.to(snap.device),
-                       j.to(snap.device))
-
-    def scaled(self, snap: torch.Tensor, factor: float) -> "Spheres":
-        return Spheres.around(snap, self.ids, self.radii * factor)
+        r = (radii.to(dev, torch.float32) * 1.0001).contiguous()
+        own_c = owner.to(dev)[ids.to(dev)]
+        n = snap.size(0)
+        cum = torch.cumsum(g.radius_counts(q, r), 0)
+        keys, start, nq = [], 0, ids.numel()
+        while start < nq:
+            base = int(cum[start - 1]) if start else 0
+            end = int(torch.searchsorted(cum, torch.tensor([base + chunk_members], device=dev), right=True))
+            end = min(max(end, start + 1), nq)
+            sl, j = g.radius(q[start:end], r[start:end])
+            keys.append(torch.unique(torch.repeat_interleave(own_c[start:end], sl.diff()) * n + j))
+            start = end
+        allk = torch.unique(torch.cat(keys))
+        rk = allk // n
+        by_rank = {int(x): (allk[rk == x] % n).to(snap.device) for x in torch.unique(rk).tolist()}
+        return Spheres(ids.to(snap.device), radii.to(snap.device, torch.float32), by_rank)
 
 
 @dataclass
@@ -119,12 +133,9 @@ class SlabPlan:
         local = []
         for r in range(world):
             inside = (key >= lo[r] - halo) & (key <= hi[r] + halo)
-            if spheres is not None and spheres.ids.numel():
-                mine = owner[spheres.ids] == r
-                if bool(mine.any()):
-                    seg = torch.repeat_interleave(mine, spheres.slices.diff())
-                    inside = inside.clone()
-                    inside[spheres.members[seg]] = True
+            if spheres is not None and r in spheres.by_rank:
+                inside = inside.clone()
+                inside[spheres.by_rank[r].to(inside.device)] = True
             local.append(torch.nonzero(inside | (owner == r)).flatten())
         return SlabPlan(world, axis, float(halo), owner, lo, hi, local, spheres)
 
@@ -479,7 +490,8 @@ class SlabDenoiser:
                 if world > 1:
                     halo, sid, srad = cut_spheres(self.snap_pos, world, k_max, quantile=sphere_quantile, weights=weights,
                                                   step=self.step_bound, horizon=self.horizon)
-                    self._spheres = Spheres.around(self.snap_pos, sid, srad) if engine_factory is None else None
+                    self._spheres = (Spheres.around(self.snap_pos, sid, srad, _cut(self.snap_pos, world, None, weights)[2])
+                                     if engine_factory is None else None)
                 else:
                     halo = 0.0
             self._lattice = (nat.grid_params(self.snap_pos.to(nat.device()), k_hint=self.k_hint)
@@ -642,10 +654,9 @@ class SlabDenoiser:
                                               query=None if state is None else state[0], iterations=at or 0,
                                               step=self.step_bound, horizon=horizon or self.horizon)
                 halo = max(band, self._band_floor, halo or 0.0)
-                self._spheres = Spheres.around(self.snap_pos, sid, srad * self._sphere_scale)
+                owner = _cut(self.snap_pos, self.t.world, self.plan.axis, self._weights)[2]
+                self._spheres = Spheres.around(self.snap_pos, sid, srad * self._sphere_scale, owner)
             else:
-                if sphere_scale is not None and self._spheres is not None:
-                    self._spheres = self._spheres.scaled(self.snap_pos, sphere_scale)
                 halo = self.plan.halo if halo is None else halo
             plan = SlabPlan.build(self.snap_pos, self.t.world, halo, axis=self.plan.axis, weights=self._weights,
                                   spheres=self._spheres)
@@ -768,6 +779,8 @@ class SlabDenoiser:
                 self._pending = []
             self._one(params)
             self.iterations_done += 1
+            if not self.step_bound:
+                self.step_bound = float(params.d)     # (the drift bound of later plans: every move is below d)
             if self.check_every > 0:
                 self._pending.append(params)
                 self._since += 1
@@ -846,36 +859,34 @@ def _quantile(x: torch.Tensor, q: float) -> float:
 def cut_spheres(snap_pos: torch.Tensor, world: int, k: int, margin: float = 1.25, quantile: float = 0.999,
                 axis: int | None = None, sphere_margin: float = 1.5, weights: torch.Tensor | None = None,
                 query: torch.Tensor | None = None, iterations: int = 0, step: float = 0.0, horizon: int = 1,
-                speed_floor: float = 0.99):
+                first_step: float = 1.75):
     """(band halo, sphere centre ids, sphere radii) for the cut SlabPlan.build makes with the same `weights` (None:
     equal counts), covering the next `horizon` iterations from the state `query` (the current positions after
-    `iterations` iterations; None: the snapshot itself).
+    `iterations` iterations; None: the snapshot itself).  step: the loop's per-iteration displacement bound d (every
+    step's move is clamped below it, Denoiser.py's `norm < d` keeps); 0 prices no drift.
 
-    Each near-face point needs its k-ball's reach past its slab's faces now, plus the drift of the iterations ahead:
-    need = reach + (horizon - 1) x v, with v its own mean speed so far (displacement from the snapshot / iterations)
-    plus a floor (the `speed_floor` quantile of those speeds: a point that has not moved yet may start to), or, before
-    any iteration, `step` (the loop's per-iteration displacement bound: every step's move is clamped below d,
-    Denoiser.py's `norm < d` keeps).  The band is `margin` x the `quantile` of the needs; every point that needs
-    more keeps a sphere around its snapshot position instead (all its snapshot members local to its owner), of
-    radius 1.1 x (displacement + d_k + twice the drift ahead) -- the triangle inequality's bound on |q - o| + d_k(q)
-    -- and at least sphere_margin x d_k.  So a few sparse or fast-moving points near a cut do not set every rank's
-    halo.  Measured on configs[4]'s 80M cloud (tools/halo_policy_probe.py, 8 slabs): planned after iteration 1 for
-    iterations 2..8 this fails no row.  A cost-weighted re-cut moves the faces, so the band and the spheres are
-    recomputed for it (SlabDenoiser._replan)."""
+    Each near-face point needs its k-ball's reach past its slab's faces now plus the growth of that reach over the
+    iterations ahead; its sphere must hold |q - o| + d_k(q) over them.  Measured on configs[4]'s 80M cloud, 8 slabs
+    (tools/halo_policy_probe.py, profiles/r6/halo_policy_probe_25_80m_r6.txt), after the first iteration, j iterations
+    ahead: both grow INDEPENDENTLY of how fast the point moved so far; the reach by ~0.16 d j at the 0.999-quantile
+    and ~2 d sqrt(j) at most, |q - o| + d_k by ~2.35 d sqrt(j) at most (j = 2 .. 23); the first iteration moves the
+    fastest points by up to 1.7 d.  So, with ahead = horizon - 1 and lead = first_step before any iteration (else 0):
+    need = reach + d (lead + 0.8 sqrt(ahead) + 0.2 ahead); the band is `margin` x the `quantile` of the needs (at least
+    the median d_k); every point that needs more keeps a sphere around its snapshot position o (all its snapshot
+    members local to its owner) of radius max(sphere_margin x d_k, 1.1 x (|q - o| + d_k + d (lead + 2.4 sqrt(ahead)))).
+    A cost-weighted re-cut moves the faces, so the band and the spheres are recomputed for it (SlabDenoiser._replan)."""
     idx, reach, dk, disp = _cut_reach(snap_pos, world, k, axis, weights, query=query)
     if idx.numel() == 0:
         z = torch.zeros(0, dtype=torch.int64)
         return 0.0, z, torch.zeros(0)
     ahead = max(int(horizon) - 1, 0)
-    if iterations > 0:
-        s = disp / float(iterations)
-        grow = ahead * (s + _quantile(s, speed_floor))
-    else:
-        grow = torch.full_like(reach, ahead * float(step))
-    need = (reach + grow).clamp(min=0)
+    lead = first_step if (iterations == 0 and ahead > 0) else 0.0
+    grow_b = float(step) * (lead + 0.8 * math.sqrt(ahead) + 0.2 * ahead)
+    grow_s = float(step) * (lead + 2.4 * math.sqrt(ahead))
+    need = (reach + grow_b).clamp(min=0)
     band = margin * max(_quantile(need, quantile), _quantile(dk, 0.5))
     out = margin * need > band
-    radii = torch.maximum(sphere_margin * dk, 1.1 * (disp + dk + 2 * grow))
+    radii = torch.maximum(sphere_margin * dk, 1.1 * (disp + dk + grow_s))
     return band, idx[out], radii[out]
 
 

@@ -27,7 +27,7 @@ def main():
     pos, nrm, _ = make_cloud(n, 3, dev)
     d = 2 * float(Processor(Pointcloud(pos), k_hint=32).meanEdgeLength())
     band, sid, srad = cut_spheres(pos, world, 32)
-    plan = SlabPlan.build(pos, world, band, spheres=Spheres.around(pos, sid, srad))
+    plan = SlabPlan.build(pos, world, band, spheres=Spheres.around(pos, sid, srad, _cut(pos, world)[2]))
     own = torch.bincount(plan.owner, minlength=world)
     halo_rows = max(int(plan.local[r].numel() - own[r]) for r in range(world))
     idx, reach0, dk0, _ = _cut_reach(pos, world, 32)

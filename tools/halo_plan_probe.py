@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "normal-guided-pointcloud-denoiser_amd"))
 sys.path.insert(0, ROOT)
 from bench import make_cloud  # noqa: E402
-from pcd_slab import SlabPlan, Spheres, cut_spheres  # noqa: E402
+from pcd_slab import SlabPlan, Spheres, _cut, cut_spheres  # noqa: E402
 
 
 def main():
@@ -21,7 +21,7 @@ def main():
     for sm in (1.25, 1.5):
         band, ids, rad = cut_spheres(pos, world, 32, sphere_margin=sm)
         for bscale, sscale in ((1.0, 1.0), (2.0, 2.0), (2.0, 1.0)):
-            sp = Spheres.around(pos, ids, rad * sscale)
+            sp = Spheres.around(pos, ids, rad * sscale, _cut(pos, world)[2])
             plan = SlabPlan.build(pos, world, band * bscale, spheres=sp)
             own = torch.bincount(plan.owner, minlength=world)
             halo = [int(plan.local[r].numel() - own[r]) for r in range(world)]

@@ -72,7 +72,7 @@ def main():
         bad_band = sum(int(((R[j] > band) & ~sph).sum()) for j in span)
         ratio = max((float(((D[j] + K[j])[sph] / rad[sph]).max()) if bool(sph.any()) else 0.0) for j in span)
         sid = idx[sph]
-        sp = Spheres.around(pos, sid, rad[sph] * 1.0) if sid.numel() else None
+        sp = Spheres.around(pos, sid, rad[sph] * 1.0, owner) if sid.numel() else None
         plan = SlabPlan.build(pos, world, band, spheres=sp)
         halo = max(int(plan.local[r].numel() - own[r]) for r in range(world))
         print(f"  {tag}: band {band:.4g} ({band / d:.2f} d), spheres {int(sph.sum()):,}, failing band rows {bad_band:,}, "
@@ -91,22 +91,17 @@ def main():
             gs = (D[j] + K[j] - K[2])[m_] / d
             row.append(f"j{j}: reach +{q(gr, 0.999):.2f}/{float(gr.max()):.2f} ball {q(gs, 0.999):.2f}/{float(gs.max()):.2f}")
         print(f"s1 in [{lo_}, {hi_}) d ({int(m_.sum()):,} rows): " + "; ".join(row), flush=True)
-    # cut_spheres' policy (g 1, floor q0.99, spheres of 1.1 x (D + d_k + rf x grow)) at band quantiles bq
-    for t, h in ((1, 7), (1, iters - 1)):
+    # cut_spheres' policy: need = reach + d (lead + 0.8 sqrt(ahead) + 0.2 ahead), spheres of 1.1 (D + d_k + d (lead + 2.4 sqrt(ahead)))
+    for t, h in ((0, 1), (0, 2), (1, 7), (1, iters - 1)):
         print(f"plan after iteration {t}, covering iterations {t + 1}..{t + h}:", flush=True)
-        need_now = R[t + 1]                 # reach at the plan's state (the query of iteration t+1)
-        k_now, d_now = K[t + 1], D[t + 1]
-        s_r = d_now / max(t, 1)
-        s_f = q(s_r, 0.99)
-        grow = (h - 1) * (s_r + s_f)
-        need = need_now + grow
-        for bq in (0.999, 0.9995, 0.9999):
-            for rf in (2.0, 1.0):
-                band = 1.25 * q(need[need > -1e8], bq)
-                sph = need > band / 1.25
-                rad = torch.maximum(1.5 * k_now, 1.1 * (d_now + k_now + rf * grow))
-                evaluate(f"band q{bq}, sphere radius 1.1 x (D + dk + {rf} grow)", t, h, band, sph, rad)
-
+        ahead = h - 1
+        lead = 1.75 if (t == 0 and ahead > 0) else 0.0
+        need = (R[t + 1] + d * (lead + 0.8 * ahead ** 0.5 + 0.2 * ahead)).clamp(min=0)
+        valid = R[t + 1] > -1e8
+        band = 1.25 * max(q(need[valid], 0.999), q(K[t + 1][valid], 0.5))
+        sph = (1.25 * need > band) & valid
+        rad = torch.maximum(1.5 * K[t + 1], 1.1 * (D[t + 1] + K[t + 1] + d * (lead + 2.4 * ahead ** 0.5)))
+        evaluate("cut_spheres", t, h, band, sph, rad)
 
 if __name__ == "__main__":
     main()
