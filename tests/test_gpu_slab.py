@@ -81,7 +81,9 @@ def _worker(rank, world, port, out_path, cloud_path, d, backend="gloo", jacobi=F
             c = np.load(cloud_path)
             pos, nrm = torch.from_numpy(c["pos"]).to(dev), torch.from_numpy(c["n"]).to(dev)
         tr = TorchTransport(rccl=backend == "rccl")
-        sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K, native=native, sphere_quantile=sq)
+        # the default halo priced for the drift of the whole run (step bound d, ITERS iterations: cut_spheres)
+        sd = SlabDenoiser(pos, nrm, max(K, KU), transport=tr, k_hint=K, native=native, sphere_quantile=sq,
+                          step_bound=d, horizon=ITERS)
         if native is not False:
             assert sd.comm.info() == {"world": world, "rank": rank,
                                       "transport": "rccl" if backend == "rccl" else "host"}
@@ -554,8 +556,8 @@ def test_cut_halo_covers_the_snapshot_balls_and_is_thinner(gpu):
 def test_hip_slab_world4_coverage_spheres_match_one_gpu(gpu, tmp_path):
     """The band halo at the MEDIAN near-face reach (sphere_quantile=0.5): half the points near a cut keep their own
     coverage sphere (every snapshot point of it local to their owner, pcd_denoiser_set_coverage_spheres), four ranks
-    sharing the GPU -- at most two re-plans as points drift out of their spheres, and the one-GPU result within
-    1e-6 x bbox."""
+    sharing the GPU -- the band and the spheres priced for the run's drift, so no re-plan (round 5 allowed two, its
+    spheres being snapshot-sized) -- and the one-GPU result within 1e-6 x bbox."""
     import torch.multiprocessing as mp
     pos, nrm = _cloud(gpu)
     d = _d(pos)
@@ -565,7 +567,7 @@ def test_hip_slab_world4_coverage_spheres_match_one_gpu(gpu, tmp_path):
     res = np.load(out)
     report(f"coverage spheres: {int(res['spheres'])} spheres, halo rows on rank 0 {int(res['halo'])}, "
            f"replans {int(res['replans'])}")
-    assert int(res["spheres"]) > 100 and int(res["replans"]) <= 2
+    assert int(res["spheres"]) > 100 and int(res["replans"]) == 0
     rp, rn = _fused(pos, nrm, d)
     bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
     np.testing.assert_allclose(res["pos"], rp, rtol=0, atol=1e-6 * bbox)
