@@ -729,6 +729,10 @@ def main():
         out["slab"] = {"world": info["world"], "transport": info["transport"],
                        "owned_rows": [int(c[0]) for c in allc], "halo_rows": [int(c[1]) for c in allc],
                        "read_rows_per_iteration": [round(r, 1) for r in read_rows] if its else None,
+                       # held = the snapshot rows a rank keeps for its kNN (sized for the planned drift); moved = the
+                       # rows the read-set exchange refreshes per iteration (what the halo costs per iteration)
+                       "halo_rows_held_max": max(int(c[1]) for c in allc),
+                       "halo_rows_moved_per_iteration_max": round(max(read_rows), 1) if its else None,
                        "readset": bool(its),
                        "halo": sd.halo, "replans": sd.replans, "replan_log": sd.replan_log,
                        "exchanges_per_iteration": (1 + 1 + (0 if params.jacobi else params.nphases - 1)) if its
