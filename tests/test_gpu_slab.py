@@ -572,3 +572,30 @@ def test_hip_slab_world4_coverage_spheres_match_one_gpu(gpu, tmp_path):
     bbox = float(np.linalg.norm(rp.max(0) - rp.min(0)))
     np.testing.assert_allclose(res["pos"], rp, rtol=0, atol=1e-6 * bbox)
     np.testing.assert_allclose(res["n"], rn, rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_sphere_members_chunked_per_owner(gpu):
+    """Spheres.around finds the members a bounded chunk of centres at a time and keeps one set per owner rank: the sets
+    equal the brute-force members (every snapshot point within 1.0001 R of a centre, unioned per centre owner) at any
+    chunk size."""
+    from pcd_slab import Spheres, _cut
+    pos, _ = _cloud(gpu)
+    owner = _cut(pos, 4)[2]
+    g = torch.Generator(device="cpu").manual_seed(3)
+    ids = torch.randperm(pos.size(0), generator=g)[:300].to(gpu)
+    radii = (0.01 + 0.03 * torch.rand(300, generator=g)).to(gpu)
+    ref = {}
+    for c, r in zip(ids.tolist(), radii.tolist()):
+        d = (pos - pos[c]).norm(dim=1)
+        m = torch.nonzero(d <= r * 1.0001).flatten()
+        o = int(owner[c])
+        ref[o] = torch.unique(torch.cat([ref.get(o, m[:0]), m]))
+    for chunk in (500, 32_000_000):
+        sp = Spheres.around(pos, ids, radii, owner, chunk_members=chunk)
+        assert sorted(sp.by_rank) == sorted(ref)
+        for o, m in ref.items():
+            got = set(sp.by_rank[o].tolist())
+            want = set(m.tolist())
+            # (the library's radius test is fp32 on squared distances: rows on the 1.0001 R shell may differ)
+            assert len(got ^ want) <= max(2, len(want) // 1000), (o, len(got ^ want))
