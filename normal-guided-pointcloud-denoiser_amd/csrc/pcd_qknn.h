@@ -199,6 +199,63 @@ PCD_DEV float rq_shrink(unsigned long long* buf, int& cnt, float capd2, const La
     return bound;
 }
 
+// The anchor set of a query with more than KA survivors, without ordering them: the largest bound b (a d²) found with
+// count(d² <= b) <= KA, by interpolation steps on [0, capd2) (survivor d² is near-uniform there: the count grows
+// with the area of the ball).  buf is compacted to the members d² <= b, in buffer order, and cnt set to their
+// count.  Every other snapshot point has fp32 d² > b, so sqrtf(b) is the set's D.  Returns false, buf untouched,
+// when no bound holding `need`..KA members was found (equal distances crowding the boundary: the query spills).
+template <int KA, int W>
+PCD_DEV bool rq_bound(unsigned long long* buf, int& cnt, float capd2, int need, float& b, const LaneGrp<W>& g) {
+    constexpr int SL = RqSurv<W>::n / W;   // slots per lane
+    wave_sync();
+    float d[SL];
+#pragma unroll
+    for (int s = 0; s < SL; ++s) {
+        const int e = s * W + g.hl;
+        d[s] = e < cnt ? __uint_as_float((uint32_t)(buf[e] >> 32)) : 3.0e38f;
+    }
+    auto count_le = [&](float t) {
+        int c = 0;
+#pragma unroll
+        for (int s = 0; s < SL; ++s)
+            if (s * W < cnt) c += __popcll(g.ballot(d[s] <= t));
+        return c;
+    };
+    float lo = 0.f, hi = capd2;
+    int clo = 0, chi = cnt, best = -1;   // (clo: a model value until lo is measured)
+#pragma unroll 1
+    for (int it = 0; it < 10; ++it) {
+        const float f = fminf(fmaxf(((float)KA + 0.5f - (float)clo) * __builtin_amdgcn_rcpf((float)max(chi - clo, 1)),
+                                    0.0625f), 0.9375f);   // (a guess: the estimate reciprocal is enough)
+        const float mid = lo + (hi - lo) * f;
+        const int c = count_le(mid);
+        if (c <= KA) {
+            lo = mid; clo = c; best = c;
+            if (c == KA) break;
+        } else {
+            hi = mid; chi = c;
+        }
+    }
+    if (best < need) return false;
+    b = lo;
+    // in-place compaction, a slot at a time: slot s's members land below (s + 1) W, never on a later slot's keys,
+    // and each slot's keys are in registers before its writes
+    const unsigned long long below = (1ull << g.hl) - 1ull;
+    int base = 0;
+#pragma unroll
+    for (int s = 0; s < SL; ++s) {
+        if (s * W >= cnt) break;
+        const bool in = d[s] <= lo;
+        const unsigned long long m = g.ballot(in);
+        const unsigned long long key = in ? buf[s * W + g.hl] : 0ull;
+        wave_sync();
+        if (in) buf[base + __popcll(m & below)] = key;
+        base += __popcll(m);
+    }
+    cnt = base;
+    return true;
+}
+
 // Cut the survivors to the K best (quantised order; K <= 2W): false when the cut is ambiguous (the query spills).
 template <int K, int W>
 PCD_DEV bool rq_cut(unsigned long long* buf, int& cnt, unsigned long long& cap, const LaneGrp<W>& g) {
@@ -422,15 +479,15 @@ PCD_DEV void rq_finish(int64_t i, Vec3 q, float r_s, int64_t N, int kstore, floa
                        bool ok, bool big, const LaneGrp<W>& lg) {
     const bool partial = cnt < KA;               // (after a buffer cut cnt == KA)
     GrpOrder<W> o{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, &lg};
+    float capd2 = __uint_as_float((unsigned)(cap >> 32)), b = -1.f;
+    const bool bounded = ok && cnt > KA;
+    // more than KA survivors: the set is every survivor under a bound (rq_bound), so only the <= KA members are
+    // ordered, for the stored list
+    if (bounded) ok = rq_bound<KA, W>(buf, cnt, capd2, kstore + 1, b, lg);
     if (ok) {
-        (void)rq_shrink<KA, W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lg);
-        ok = cnt <= 4 * W;                        // (a set that did not shrink to 4W spills)
-    }
-    if (ok) {
-        o = grp_order32<W>(buf, cnt, __uint_as_float((unsigned)(cap >> 32)), lg);
-        // exact order of the stored list (first kstore + its successor) and of the anchor set boundary
+        o = grp_order32<W>(buf, cnt, bounded ? b : capd2, lg);
+        // exact order of the stored list (first kstore + its successor)
         ok = order_exact<W>(o, kstore, lg);
-        ok = ok && (cnt <= KA || (o.at(KA) >> 8) != (o.at(KA - 1) >> 8));
     }
     if (!ok) {
         wave_sync();
@@ -440,33 +497,27 @@ PCD_DEV void rq_finish(int64_t i, Vec3 q, float r_s, int64_t N, int kstore, floa
         }
         return;
     }
-    // this lane's elements hl and W + hl of the order; unused slots of a partial set hold N, the snapshot's +inf sentinel row (the anchor test
-    // gives them an infinite distance)
+    // the stored list: the first kstore of the order, whole 32-B sectors of the blocked list layout (pcd_lists.h):
+    // lanes 8b .. 8b+7 fill block b of row i
     const int e0 = lg.hl, e1 = W + lg.hl;
-    const bool h0 = e0 < KA && e0 < cnt, h1 = e1 < KA && e1 < cnt;
-    const unsigned long long m0 = h0 ? buf[o.s0 & 255u] : 0ull;
-    const unsigned long long m1 = h1 ? buf[o.s1 & 255u] : 0ull;
-    const int32_t r0 = h0 ? (int32_t)(uint32_t)(m0 & 0xFFFFFFFFull) : (int32_t)N;   // N: the +inf sentinel row
-    const int32_t r1 = h1 ? (int32_t)(uint32_t)(m1 & 0xFFFFFFFFull) : (int32_t)N;
-    // whole 32-B sectors of the blocked list layout (pcd_lists.h): lanes 8b .. 8b+7 fill block b of row i
-    if (e0 < kstore) idx[lpos(N, i, e0)] = r0;
-    if (e1 < kstore) idx[lpos(N, i, e1)] = r1;
-    // the anchor set is stored in RANK order (unused slots last): the anchor test ranks it by distance itself,
-    // and neighbouring rows -- neighbouring lanes of its waves -- then gather nearly the same snapshot rows in the
-    // same slot, i.e. the same cache lines, instead of 64 unrelated ones per gather instruction
-    {
-        constexpr int M = KA > W ? 2 : 1;
-        uint32_t v[M];
-        v[0] = e0 < KA ? (uint32_t)r0 : 0xFFFFFFFFu;
-        if (M > 1) v[M - 1] = e1 < KA ? (uint32_t)r1 : 0xFFFFFFFFu;
-        grp_bitonic_sort32<W, M>(v, lg.hl);
-        if (e0 < KA) alist[lpos(N, i, e0)] = (int32_t)v[0];
-        if (M > 1 && e1 < KA) alist[lpos(N, i, e1)] = (int32_t)v[M - 1];
-    }
-    // D: the KA-th distance = the largest exact d² of the anchor set (quantised ties inside it are harmless); for
-    // a partial set, r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7))
-    const unsigned long long mx = grp_max_u64<W>(m0 > m1 ? m0 : m1);
-    const float D = partial ? r_s * (1.f - 1e-6f) : sqrtf(__uint_as_float((unsigned)(mx >> 32)));
+    if (e0 < kstore) idx[lpos(N, i, e0)] = (int32_t)(uint32_t)(buf[o.s0 & 255u] & 0xFFFFFFFFull);
+    if (e1 < kstore) idx[lpos(N, i, e1)] = (int32_t)(uint32_t)(buf[o.s1 & 255u] & 0xFFFFFFFFull);
+    // the anchor set: every survivor left in buf (cnt <= KA), in BUFFER order, i.e. the scan's: cells in (z, y, x)
+    // order of the box, ranks ascending inside a cell -- one global order, so neighbouring rows (neighbouring lanes
+    // of the anchor test's waves) hold mostly the same snapshot rows at the same slot and gather the same cache
+    // lines.  (It was rank order, by a 64-key sort here; the anchor test ranks the set by distance itself.)  Unused
+    // slots of a partial set hold N, the snapshot's +inf sentinel row (the anchor test gives them an infinite
+    // distance).
+    const unsigned long long m0 = e0 < cnt ? buf[e0] : 0ull, m1 = e1 < cnt ? buf[e1] : 0ull;
+    if (e0 < KA) alist[lpos(N, i, e0)] = e0 < cnt ? (int32_t)(uint32_t)(m0 & 0xFFFFFFFFull) : (int32_t)N;
+    if (e1 < KA) alist[lpos(N, i, e1)] = e1 < cnt ? (int32_t)(uint32_t)(m1 & 0xFFFFFFFFull) : (int32_t)N;
+    // D: every snapshot point outside the set is at least D from q.  Bounded set: sqrtf(b) (rq_bound); a partial
+    // set: r (rounded down: a point outside has fp32 d² > r², true distance > r (1 - 1e-7)); exactly KA survivors
+    // (a buffer cut's, or the ball's own): the largest exact d² of the set (an outside point's 64-bit key is larger)
+    float D;
+    if (bounded) D = sqrtf(b);
+    else if (partial) D = r_s * (1.f - 1e-6f);
+    else D = sqrtf(__uint_as_float((unsigned)(grp_max_u64<W>(m0 > m1 ? m0 : m1) >> 32)));
     if (lg.hl == 0) anc[i] = make_float4(q.x, q.y, q.z, D);
 }
 
