@@ -100,7 +100,8 @@ struct GrpOrder {
         return e < W ? g->bcast(s0, e) : g->bcast(s1, e - W);
     }
 };
-template <int W>
+// MS: the most slots a caller's set can fill (cnt <= MS * W; 1 or 2 drop the larger networks from the code)
+template <int W, int MS = 4>
 PCD_DEV GrpOrder<W> grp_order32(const unsigned long long* buf, int cnt, float capd2, const LaneGrp<W>& g) {
     wave_sync();
     const float S = 16777216.f / fmaxf(capd2, 1e-30f);
@@ -111,11 +112,11 @@ PCD_DEV GrpOrder<W> grp_order32(const unsigned long long* buf, int cnt, float ca
     };
     const int hl = g.hl;
     GrpOrder<W> o{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, &g};
-    if (cnt <= W) {
+    if (MS == 1 || cnt <= W) {
         uint32_t v[1] = {k32(hl)};
         grp_bitonic_sort32<W, 1>(v, hl);
         o.s0 = v[0];
-    } else if (cnt <= 2 * W) {
+    } else if (MS == 2 || cnt <= 2 * W) {
         uint32_t v[2] = {k32(hl), k32(W + hl)};
         grp_bitonic_sort32<W, 2>(v, hl);
         o.s0 = v[0]; o.s1 = v[1];
@@ -485,7 +486,7 @@ PCD_DEV void rq_finish(int64_t i, Vec3 q, float r_s, int64_t N, int kstore, floa
     // ordered, for the stored list
     if (bounded) ok = rq_bound<KA, W>(buf, cnt, capd2, kstore + 1, b, lg);
     if (ok) {
-        o = grp_order32<W>(buf, cnt, bounded ? b : capd2, lg);
+        o = grp_order32<W, (KA + W - 1) / W>(buf, cnt, bounded ? b : capd2, lg);   // (cnt <= KA here)
         // exact order of the stored list (first kstore + its successor)
         ok = order_exact<W>(o, kstore, lg);
     }
@@ -802,17 +803,28 @@ __global__ __launch_bounds__(256, PCD_DQ_OCC) void k_knn_dense_q(GridView g, con
         else
             for (int j = 0; j < Q; ++j) clean[j] = false;   // (the union is too wide: every query alone)
         (void)any_big;
-#pragma unroll
+        // the finishes one query at a time through ONE copy of the finish and of the lone re-run (not unrolled: the
+        // query's state is picked by wave-uniform selects; half the kernel's code, measured neutral in time)
+#pragma unroll 1
         for (int j = 0; j < Q; ++j) {
-            if (!act[j]) continue;
-            if (clean[j] && cnt[j] > kstore) {
-                rq_finish<KA, W>(iq[j], q[j], rs[j], N, kstore, anc, alist, idx, spill, spill_cnt, bufs[j], cnt[j],
-                                 cap[j], true, false, lg);
+            bool aj = act[0], cj = clean[0];
+            int64_t ij = iq[0];
+            Vec3 qj = q[0];
+            float rj = rs[0];
+            int nj = cnt[0];
+            unsigned long long capj = cap[0];
+#pragma unroll
+            for (int u = 1; u < Q; ++u)
+                if (j == u) { aj = act[u]; cj = clean[u]; ij = iq[u]; qj = q[u]; rj = rs[u]; nj = cnt[u]; capj = cap[u]; }
+            if (!aj) continue;
+            unsigned long long* bj = s_buf[wv][j];
+            if (cj && nj > kstore) {
+                rq_finish<KA, W>(ij, qj, rj, N, kstore, anc, alist, idx, spill, spill_cnt, bj, nj, capj, true, false, lg);
             } else {
                 // alone: its own box (an oversized one spills in there), the radius widened when too few were found
                 wave_sync();
-                (void)rq_query<KA, W>(g, GridSrc{&g}, iq[j], q[j], clean[j] ? rs[j] * 1.6f : rs[j], N, kstore, anc,
-                                      alist, idx, spill, spill_cnt, bufs[j], &s_cells[wv], lg);
+                (void)rq_query<KA, W>(g, GridSrc{&g}, ij, qj, cj ? rj * 1.6f : rj, N, kstore, anc, alist, idx, spill,
+                                      spill_cnt, bj, &s_cells[wv], lg);
             }
             wave_sync();
         }
