@@ -299,11 +299,19 @@ static constexpr int kRqChunkLog2 = kRqChunk == 64 ? 6 : kRqChunk == 128 ? 7 : 8
 #define PCD_RQ_MAP 1024        // flattened rows of a chunk mapped to their cell in LDS (0: binary search per row)
 #endif
 static constexpr int kRqMap = PCD_RQ_MAP;
+#ifndef PCD_RQ_ROWMAP
+#define PCD_RQ_ROWMAP 512      // > 0: the map holds each flattened row's snapshot row itself (one LDS read per row)
+#endif
+static constexpr int kRqRowMap = PCD_RQ_ROWMAP;
 struct RqCells {            // per-group LDS scratch for one chunk of cells
     uint32_t start[kRqChunk];
     uint32_t end_incl[kRqChunk];
-    uint8_t cellof[kRqMap > 0 ? kRqMap : 4];   // cell (slot in the chunk) of each flattened candidate row
+    uint8_t cellof[kRqRowMap > 0 ? 4 : (kRqMap > 0 ? kRqMap : 4)];   // cell (slot in the chunk) of each flattened candidate row
+    uint32_t rowof[kRqRowMap > 0 ? kRqRowMap : 1];                    // or its snapshot row
 };
+PCD_DEV void fill_rowof(uint32_t* rowof, uint32_t b, uint32_t e, uint32_t s) {
+    for (uint32_t k = b; k < e; ++k) rowof[k] = s + (k - b);
+}
 // cellof[b..e) = v, a byte at a time (whole 32-bit words between the ends measured slower: DESIGN.md §3)
 PCD_DEV void fill_cellof(uint8_t* cellof, uint32_t b, uint32_t e, uint32_t v) {
     for (uint32_t k = b; k < e; ++k) cellof[k] = (uint8_t)v;
@@ -409,11 +417,13 @@ PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo
         }
         // the cell of every flattened row, so a row finds its cell with one LDS read instead of a binary search over
         // the chunk (~40 VALU per row): each lane fills the runs of its own cells
-        const bool mapped = kRqMap > 0 && total <= (uint32_t)kRqMap;   // (group-uniform)
+        const bool mapped = kRqRowMap > 0 ? total <= (uint32_t)kRqRowMap : kRqMap > 0 && total <= (uint32_t)kRqMap;
         if (mapped) {
 #pragma unroll
-            for (int u = 0; u < CPL; ++u)
-                fill_cellof(wc->cellof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], (uint32_t)(hl * CPL + u));
+            for (int u = 0; u < CPL; ++u) {
+                if (kRqRowMap > 0) fill_rowof(wc->rowof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], cr[u].x);
+                else fill_cellof(wc->cellof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], (uint32_t)(hl * CPL + u));
+            }
         }
         wave_sync();
         for (uint32_t j0 = 0; j0 < total; j0 += W * kRqRows) {
@@ -423,6 +433,10 @@ PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo
 #pragma unroll
             for (int u = 0; u < kRqRows; ++u) {
                 const uint32_t j = j0 + (uint32_t)(u * W + hl);
+                if (kRqRowMap > 0 && mapped) {
+                    r[u] = j < total ? wc->rowof[j] : 0u;
+                    continue;
+                }
                 int a = 0;
                 if (mapped) {
                     a = j < total ? (int)wc->cellof[j] : 0;
@@ -659,11 +673,13 @@ PCD_DEV void rq_scan_box_q(const GridView& g, const Src& src, const Vec3 (&q)[Q]
             wc->start[hl * CPL + u] = cr[u].x;
             wc->end_incl[hl * CPL + u] = excl + loc[u];
         }
-        const bool mapped = kRqMap > 0 && total <= (uint32_t)kRqMap;
+        const bool mapped = kRqRowMap > 0 ? total <= (uint32_t)kRqRowMap : kRqMap > 0 && total <= (uint32_t)kRqMap;
         if (mapped) {
 #pragma unroll
-            for (int u = 0; u < CPL; ++u)
-                fill_cellof(wc->cellof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], (uint32_t)(hl * CPL + u));
+            for (int u = 0; u < CPL; ++u) {
+                if (kRqRowMap > 0) fill_rowof(wc->rowof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], cr[u].x);
+                else fill_cellof(wc->cellof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], (uint32_t)(hl * CPL + u));
+            }
         }
         wave_sync();
         for (uint32_t j0 = 0; j0 < total; j0 += W * kRqRows) {
@@ -675,6 +691,10 @@ PCD_DEV void rq_scan_box_q(const GridView& g, const Src& src, const Vec3 (&q)[Q]
 #pragma unroll
             for (int u = 0; u < kRqRows; ++u) {
                 const uint32_t jj = j0 + (uint32_t)(u * W + hl);
+                if (kRqRowMap > 0 && mapped) {
+                    r[u] = jj < total ? wc->rowof[jj] : 0u;
+                    continue;
+                }
                 int a = 0;
                 if (mapped) {
                     a = jj < total ? (int)wc->cellof[jj] : 0;
