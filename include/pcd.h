@@ -231,7 +231,8 @@ int pcd_denoiser_tile_stats(pcd_denoiser* dn, int64_t* out4, void* stream);
  * stages; get_timing returns each stage's elapsed ms AVERAGED over the iterations recorded since set_timing or
  * the previous get_timing, then starts over.  Slots: anchor test (+ redo-list select), re-anchoring search, exact-key
  * spill search, NVT1 (the four make up K1: kNN + NVT1; a non-anchored K1 reports its whole time in the NVT1 slot),
- * NVT2, phase 0, phase 1, phase 2, finish, -. */
+ * NVT2, phase 0, phase 1, phase 2, finish, -.  enable = 2 records the K1 stage's two events only (one slot: K1's
+ * ms), for a timed region that needs K1's time without the other stages' events (~4 us each on the stream). */
 int pcd_denoiser_set_timing(pcd_denoiser* dn, int enable);
 int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n_written);
 /* Device error word -> status: PCD_ERR_STATE if a kNN list held an invalid entry or (spatial slabs) a query's

@@ -990,6 +990,7 @@ struct pcd_denoiser {
     float4* probe = nullptr;      // NVT2 parity probe (pcd_denoiser_set_probe): normalised eigenvalues + Σw per row
     bool loaded = false, iterated = false;
     bool timing = false;
+    bool timing_k1 = false;       // level 2: only the K1 stage's two events (the bench's timed region)
     std::vector<hipEvent_t> ev;   // kTimingSets sets of kTimingEvents events, one set per timed iteration
     int ev_used = 0;              // sets recorded since set_timing / the last get_timing
     // spatial slabs (pcd_slab.h): halo routes, band flags, the exchange stream and the exchange in flight
@@ -1625,6 +1626,7 @@ int pcd_denoiser_set_seeding(pcd_denoiser* dn, int enable) {
 int pcd_denoiser_set_timing(pcd_denoiser* dn, int enable) {
     PCD_CHECK_ARG(dn != nullptr, "null denoiser");
     dn->timing = enable != 0;
+    dn->timing_k1 = enable == 2;
     dn->ev_used = 0;
     if (dn->timing && dn->ev.empty()) {
         dn->ev.resize((size_t)kTimingSets * kTimingEvents);
@@ -1638,8 +1640,22 @@ int pcd_denoiser_get_timing(pcd_denoiser* dn, float* ms_out, int n_slots, int* n
     *n_written = 0;
     if (!dn->timing || dn->ev.empty() || dn->ev_used == 0) return PCD_OK;
     const int sets = dn->ev_used;
-    PCD_HIP(hipEventSynchronize(dn->ev[(size_t)(sets - 1) * kTimingEvents + kTimingEvents - 1]));
     int w = 0;
+    if (dn->timing_k1) {                  // one slot: the K1 stage (events 0 and 4 of each set)
+        PCD_HIP(hipEventSynchronize(dn->ev[(size_t)(sets - 1) * kTimingEvents + 4]));
+        double acc = 0.0;
+        for (int st = 0; st < sets && n_slots > 0; ++st) {
+            float m = 0.f;
+            hipEvent_t* e = &dn->ev[(size_t)st * kTimingEvents];
+            PCD_HIP(hipEventElapsedTime(&m, e[0], e[4]));
+            acc += m;
+        }
+        if (n_slots > 0) ms_out[w++] = (float)(acc / sets);
+        *n_written = w;
+        dn->ev_used = 0;
+        return PCD_OK;
+    }
+    PCD_HIP(hipEventSynchronize(dn->ev[(size_t)(sets - 1) * kTimingEvents + kTimingEvents - 1]));
     for (int slot = 0; slot + 1 < kTimingEvents && w < n_slots; ++slot) {
         double acc = 0.0;
         for (int st = 0; st < sets; ++st) {
@@ -1664,8 +1680,9 @@ int pcd_denoiser_iterate(pcd_denoiser* dn, const pcd_denoise_params* p, int iter
         hipEvent_t* ev = nullptr;     // this iteration's event set (timing on, and a set left)
         if (dn->timing && dn->ev_used < kTimingSets) ev = &dn->ev[(size_t)dn->ev_used++ * kTimingEvents];
         if (ev) PCD_HIP(hipEventRecord(ev[0], st));
-        if ((rc = stage_k1(dn, p, st, ev)) != PCD_OK) return rc;
+        if ((rc = stage_k1(dn, p, st, dn->timing_k1 ? nullptr : ev)) != PCD_OK) return rc;
         if (ev) PCD_HIP(hipEventRecord(ev[4], st));
+        if (dn->timing_k1) ev = nullptr;   // (level 2: K1 only)
         if ((rc = stage_k2(dn, p, st)) != PCD_OK) return rc;
         if (ev) PCD_HIP(hipEventRecord(ev[5], st));
         // copy-free phases when three Gauss-Seidel phases move the three classes of every row once each and only the

@@ -385,7 +385,8 @@ class FusedDenoiser:
     def reset_seed(self):
         check(lib().pcd_denoiser_reset_seed(self.handle), "pcd_denoiser_reset_seed")
 
-    def set_timing(self, on: bool):
+    def set_timing(self, on):
+        """False / True: off / every stage (TIMING_SLOTS); 2: the K1 stage only (one slot, K1's ms)."""
         check(lib().pcd_denoiser_set_timing(self.handle, int(on)), "pcd_denoiser_set_timing")
 
     def check(self):
