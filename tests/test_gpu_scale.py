@@ -208,3 +208,32 @@ def test_config3_170k_k32_twenty_iterations(gpu):
         c_ref = float(O.chamfer(v, p).mean())
         c_gpu = float(O.chamfer(v, pc.v.cpu().numpy()).mean())
         assert abs(c_gpu - c_ref) <= 2e-3 * c_ref, (c_gpu, c_ref)
+
+
+def test_k1_only_timing_level(gpu):
+    """pcd_denoiser_set_timing(2), the bench's timed region: one slot (K1's ms), consistent with the full split's K1
+    slots on a replay of the same iterations, and timing changes no result (state bitwise equal either way)."""
+    pos, nrm = bunny_cloud(400_000, 5, 0.005)
+    pc = Pointcloud(pos.to(gpu), nrm.to(gpu))
+    proc = Processor(pc, k_hint=32)
+    params = nat.make_params(k=32, k_update=8, d=2 * float(proc.meanEdgeLength()))
+    fused = proc._fused_for(32)
+    out = []
+    for level in (2, True):
+        fused.load(proc.graph.pos, proc.graph.n)
+        fused.reset_seed()
+        fused.iterate(params, 3)
+        fused.set_timing(level)
+        fused.iterate(params, 5)
+        slots = fused.timing()
+        fused.set_timing(False)
+        p, n = torch.empty_like(pc.v), torch.empty_like(pc.v)
+        fused.store(p, n)
+        out.append((slots, p, n))
+    (k1, p2, n2), (full, p1, n1) = out
+    assert len(k1) == 1 and k1[0] > 0, k1
+    assert len(full) >= len(nat.FusedDenoiser.TIMING_SLOTS), full   # (+ the trailing "-" slot)
+    k1_full = sum(full[:4])
+    report(f"K1 ms: K1-only events {k1[0]:.4f}, full split {k1_full:.4f} (400k points, iterations 4-8)")
+    assert 0.5 * k1_full < k1[0] < 2.0 * k1_full
+    assert torch.equal(p1, p2) and torch.equal(n1, n2)
