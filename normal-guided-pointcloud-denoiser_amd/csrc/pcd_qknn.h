@@ -295,26 +295,17 @@ static constexpr int kRqMaxCells = 4096;
 static constexpr int kRqChunk = PCD_RQ_CELLS;  // cells per chunk (per group)
 template <int W> struct RqCPL { static constexpr int n = kRqChunk / W; };   // cells per lane per chunk
 static constexpr int kRqChunkLog2 = kRqChunk == 64 ? 6 : kRqChunk == 128 ? 7 : 8;
-#ifndef PCD_RQ_MAP
-#define PCD_RQ_MAP 1024        // flattened rows of a chunk mapped to their cell in LDS (0: binary search per row)
-#endif
-static constexpr int kRqMap = PCD_RQ_MAP;
-#ifndef PCD_RQ_ROWMAP
-#define PCD_RQ_ROWMAP 512      // > 0: the map holds each flattened row's snapshot row itself (one LDS read per row)
-#endif
-static constexpr int kRqRowMap = PCD_RQ_ROWMAP;
+// A chunk's flattened candidate rows mapped to their snapshot rows in LDS, so a row costs one LDS read (round 6; it
+// was the row's cell slot, a byte, then that cell's start and offset: three dependent reads).  A chunk with more
+// flattened rows than the map holds finds each row's cell by a binary search over the chunk instead.
+static constexpr int kRqRowMap = 512;
 struct RqCells {            // per-group LDS scratch for one chunk of cells
     uint32_t start[kRqChunk];
     uint32_t end_incl[kRqChunk];
-    uint8_t cellof[kRqRowMap > 0 ? 4 : (kRqMap > 0 ? kRqMap : 4)];   // cell (slot in the chunk) of each flattened candidate row
-    uint32_t rowof[kRqRowMap > 0 ? kRqRowMap : 1];                    // or its snapshot row
+    uint32_t rowof[kRqRowMap];   // snapshot row of each flattened candidate row
 };
 PCD_DEV void fill_rowof(uint32_t* rowof, uint32_t b, uint32_t e, uint32_t s) {
     for (uint32_t k = b; k < e; ++k) rowof[k] = s + (k - b);
-}
-// cellof[b..e) = v, a byte at a time (whole 32-bit words between the ends measured slower: DESIGN.md §3)
-PCD_DEV void fill_cellof(uint8_t* cellof, uint32_t b, uint32_t e, uint32_t v) {
-    for (uint32_t k = b; k < e; ++k) cellof[k] = (uint8_t)v;
 }
 // Where a scan reads its cells and candidate rows from: GridSrc is the grid in global memory (brick hash probes,
 // brick cell blocks, snapshot rows; a row's rank is its index).  A source only has to resolve a lane's cells to row
@@ -417,13 +408,11 @@ PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo
         }
         // the cell of every flattened row, so a row finds its cell with one LDS read instead of a binary search over
         // the chunk (~40 VALU per row): each lane fills the runs of its own cells
-        const bool mapped = kRqRowMap > 0 ? total <= (uint32_t)kRqRowMap : kRqMap > 0 && total <= (uint32_t)kRqMap;
+        const bool mapped = total <= (uint32_t)kRqRowMap;   // (group-uniform)
         if (mapped) {
 #pragma unroll
-            for (int u = 0; u < CPL; ++u) {
-                if (kRqRowMap > 0) fill_rowof(wc->rowof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], cr[u].x);
-                else fill_cellof(wc->cellof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], (uint32_t)(hl * CPL + u));
-            }
+            for (int u = 0; u < CPL; ++u)
+                fill_rowof(wc->rowof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], cr[u].x);
         }
         wave_sync();
         for (uint32_t j0 = 0; j0 < total; j0 += W * kRqRows) {
@@ -433,20 +422,15 @@ PCD_DEV bool rq_scan_box(const GridView& g, const Src& src, Vec3 q, const int lo
 #pragma unroll
             for (int u = 0; u < kRqRows; ++u) {
                 const uint32_t j = j0 + (uint32_t)(u * W + hl);
-                if (kRqRowMap > 0 && mapped) {
+                if (mapped) {
                     r[u] = j < total ? wc->rowof[j] : 0u;
                     continue;
                 }
-                int a = 0;
-                if (mapped) {
-                    a = j < total ? (int)wc->cellof[j] : 0;
-                } else {
-                    int b = kRqChunk - 1;
+                int a = 0, b = kRqChunk - 1;
 #pragma unroll
-                    for (int it = 0; it < kRqChunkLog2; ++it) {
-                        const int m = (a + b) >> 1;
-                        if (wc->end_incl[m] > j) b = m; else a = m + 1;
-                    }
+                for (int it = 0; it < kRqChunkLog2; ++it) {
+                    const int m = (a + b) >> 1;
+                    if (wc->end_incl[m] > j) b = m; else a = m + 1;
                 }
                 r[u] = j < total ? wc->start[a] + (j - (a ? wc->end_incl[a - 1] : 0u)) : 0u;
             }
@@ -673,13 +657,11 @@ PCD_DEV void rq_scan_box_q(const GridView& g, const Src& src, const Vec3 (&q)[Q]
             wc->start[hl * CPL + u] = cr[u].x;
             wc->end_incl[hl * CPL + u] = excl + loc[u];
         }
-        const bool mapped = kRqRowMap > 0 ? total <= (uint32_t)kRqRowMap : kRqMap > 0 && total <= (uint32_t)kRqMap;
+        const bool mapped = total <= (uint32_t)kRqRowMap;   // (group-uniform)
         if (mapped) {
 #pragma unroll
-            for (int u = 0; u < CPL; ++u) {
-                if (kRqRowMap > 0) fill_rowof(wc->rowof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], cr[u].x);
-                else fill_cellof(wc->cellof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], (uint32_t)(hl * CPL + u));
-            }
+            for (int u = 0; u < CPL; ++u)
+                fill_rowof(wc->rowof, excl + (u ? loc[u - 1] : 0u), excl + loc[u], cr[u].x);
         }
         wave_sync();
         for (uint32_t j0 = 0; j0 < total; j0 += W * kRqRows) {
@@ -691,20 +673,15 @@ PCD_DEV void rq_scan_box_q(const GridView& g, const Src& src, const Vec3 (&q)[Q]
 #pragma unroll
             for (int u = 0; u < kRqRows; ++u) {
                 const uint32_t jj = j0 + (uint32_t)(u * W + hl);
-                if (kRqRowMap > 0 && mapped) {
+                if (mapped) {
                     r[u] = jj < total ? wc->rowof[jj] : 0u;
                     continue;
                 }
-                int a = 0;
-                if (mapped) {
-                    a = jj < total ? (int)wc->cellof[jj] : 0;
-                } else {
-                    int b = kRqChunk - 1;
+                int a = 0, b = kRqChunk - 1;
 #pragma unroll
-                    for (int it = 0; it < kRqChunkLog2; ++it) {
-                        const int m = (a + b) >> 1;
-                        if (wc->end_incl[m] > jj) b = m; else a = m + 1;
-                    }
+                for (int it = 0; it < kRqChunkLog2; ++it) {
+                    const int m = (a + b) >> 1;
+                    if (wc->end_incl[m] > jj) b = m; else a = m + 1;
                 }
                 r[u] = jj < total ? wc->start[a] + (jj - (a ? wc->end_incl[a - 1] : 0u)) : 0u;
             }
