@@ -58,11 +58,12 @@ TRAFFIC_KIND = ("L2-miss bytes per launch: rocprofv3 FETCH_SIZE x 2 (gfx950 corr
                 "hits included, so an upper bound on HBM traffic")
 
 
-# Per-stage bound, as the rocprofv3 counters of profiles/ show it: VALU = VALU-issue-bound (>= 1/2 of
-# the SIMD's VALU issue busy), latency = memory-latency-bound (SQ wait > 0.6 of wave cycles at full occupancy).
-STAGE_BOUND = {"anchor_test": "valu", "requery": "latency+valu", "spill_search": "latency", "nvt1": "valu",
-               "nvt2": "valu", "flat_phase": "latency", "edge_phase": "latency", "corner_phase": "latency",
-               "finish": "-"}
+# Per-stage bound, as the rocprofv3 counters of profiles/ show it, VALU issue priced at gfx950's 2
+# cycles per wave64 instruction: valu = the SIMD's VALU issue busy >= ~1/2 of the kernel, latency = waves parked on
+# memory most of the time, ta = the texture addresser busy (one cycle per active lane of a gather).
+STAGE_BOUND = {"anchor_test": "ta (64 row gathers a row)", "requery": "latency", "spill_search": "latency",
+               "nvt1": "valu+latency", "nvt2": "latency+valu", "flat_phase": "latency", "edge_phase": "latency",
+               "corner_phase": "latency", "finish": "-"}
 
 
 def cpu_model():
@@ -704,7 +705,7 @@ def main():
                                "unit": "GB/s",
                                "frac": round(iter_alg / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
         "measured_traffic": measured_traffic(args.points, args.k, ms_per_step) if mode != "slab" else None,
-        "roofline": {"kernel": "K1 stage (kNN + NVT1): " + " + ".join(k1_names), "bound": "valu+latency",
+        "roofline": {"kernel": "K1 stage (kNN + NVT1): " + " + ".join(k1_names), "bound": "latency+ta+valu",
                      "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                      "traffic": traffic, "traffic_kind": TRAFFIC_KIND, "traffic_build": traffic_build,
