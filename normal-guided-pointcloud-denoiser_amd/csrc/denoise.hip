@@ -599,7 +599,8 @@ __global__ __launch_bounds__(256, PCD_REDO_OCC) void k_knn_redo_wave(GridView g,
         const bool all_valid = !__any(lane < KA && !valid);
         if (!all_valid && lane == 0) atomicOr(err, 1);
         if (lane < kstore) idx[lpos(N, i, lane)] = r;   // (whole 32-B sectors, pcd_lists.h)
-        {   // the anchor set in rank order (see k_knn_requery), unused slots last
+        {   // the anchor set in rank order (a consistent order for the anchor test's gathers, like the re-anchoring
+            // search's scan order, rq_finish), unused slots last
             uint32_t v[1] = {lane < KA ? (uint32_t)r : 0xFFFFFFFFu};
             grp_bitonic_sort32<64, 1>(v, lane);
             if (lane < KA) alist[lpos(N, i, lane)] = (int32_t)v[0];

@@ -8,9 +8,11 @@
 //     ORDERED by 32-bit keys floor(d² · 2^24 / cap d²) << 8 | buffer slot: a compare-exchange is one min + one max
 //     on one register and one cross-lane move, where the exact keys need two registers, two moves, a 64-bit compare
 //     and four selects (the sort was ~65 % of the old kernel's VALU).  The quantised order is the exact order
-//     wherever neighbouring quantised values differ; a query whose anchor set (first KA) or stored list (first
-//     kstore + 1) has two equal quantised values at a decision point is SPILLED to the exact-key wave search
-//     (k_knn_redo_wave), so the lists stay bit-identical to it;
+//     wherever neighbouring quantised values differ; a query whose stored list (first kstore + 1) has two equal
+//     quantised values at a decision point is SPILLED to the exact-key wave search (k_knn_redo_wave), so the lists
+//     stay bit-identical to it;
+//   * the anchor set is not ordered: with more than KA survivors it is every survivor under an exact d² bound found
+//     by a few ballot-counted interpolation steps (rq_bound), kept in the scan's order;
 //   * a full buffer is cut to the KA best the same way (the cap tightens to the largest kept exact key + 1).
 // The first iteration (no anchors yet, k_knn_dense_q): the radius is r_scale · h · (16 / n)^(1/3), n = occupancy of
 // the query's cell; a query with too few points inside it is widened, then spilled (the wave search grows its own box).
@@ -469,7 +471,7 @@ struct RqStats { unsigned redo_cnt, spill_cnt, spill_big, spill_amb; };
 #define PCD_RQ_OCC 8
 #endif
 // The end of a re-anchoring query once its survivors are in buf[0..cnt) under cap: the exact order checks, then the
-// stored list, the anchor set (rank order) and the anchor -- or the spill list when a check fails (ok = false on
+// stored list, the anchor set (scan order) and the anchor -- or the spill list when a check fails (ok = false on
 // entry: the scan was ambiguous or found too few points).
 template <int KA, int W>
 PCD_DEV void rq_finish(int64_t i, Vec3 q, float r_s, int64_t N, int kstore, float4* __restrict__ anc,
